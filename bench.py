@@ -1,0 +1,261 @@
+"""Device-resident packet-path benchmark (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config parse64|imix|imix_csum|nat64]
+
+A step is one pass of the hot path over one batch of synthetic packets that
+is already resident in HBM.  Default workload = BASELINE config 2 with the
+north-star feature set: 1,048,576 x 64-B Ethernet/IPv4/UDP frames, parse +
+IPv4 header checksum + UDP checksum verify + 5-tuple flow hash, one
+`cgpu_parse_batch` launch per step.  To keep the measurement an HBM one, each
+rank keeps R copies of its batch at different HBM addresses (R x 70 MB >
+the 256 MiB Infinity Cache) and step k processes copy k mod R.
+
+Multi-GPU (torch.distributed.run, one process per GPU): every rank owns an
+independent RX-queue shard (its own seed, its own HBM) -- no data-path
+collective, weak scaling; the process group only carries the barriers and the
+max-over-ranks of the elapsed time.  value = packets processed by all ranks /
+that time.
+
+Rank 0 prints ONE JSON line with `roofline` (dominant kernel, per-launch HIP
+event timing on the launch stream) and, at N=1, `cpu_baseline` (the C oracle
+restatement of the same workload timed on a bounded sample on one host core).
+"""
+import argparse
+import ctypes
+import json
+import os
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+INFINITY_CACHE = 256 << 20
+
+
+def header_bytes(meta):
+    """Bytes of the headers the reference touches per packet:
+    eth 14/18/22 + L3 20/40 + L4 8/20."""
+    eth = (meta >> 8) & 0xFF
+    l3 = np.where(((meta >> 16) & 3) == 2, 40, 20)
+    l4 = np.where(((meta >> 18) & 3) == 1, 8, 20)
+    return eth + l3 + l4
+
+
+def make_workload(cfg, seed):
+    from capsule_amd import _native as N
+    from capsule_amd import synth
+
+    n = 1 << 20
+    if cfg == "parse64":
+        arena, off, ln = synth.uniform(n, seed=seed)
+        flags = N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP | N.F_CSUM_L4 | N.F_FLOW_HASH
+        desc = "1M x 64B Eth/IPv4/UDP: parse + IPv4/UDP checksum verify + 5-tuple hash"
+        return dict(arena=arena, off=off, len=ln, flags=flags, kind="parse", desc=desc,
+                    algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame="64B")
+    if cfg == "imix":
+        return imix_header_bytes_workload(seed)
+    if cfg == "imix_csum":
+        arena, off, ln = synth.imix(n, seed=seed)
+        flags = N.F_ACCEPT_ALL | N.F_FLOW_HASH | N.F_CSUM_IP | N.F_CSUM_L4
+        desc = "1M IMIX 64/570/1500 7:4:1 v4/v6 x UDP/TCP: parse + checksums + hash"
+        return dict(arena=arena, off=off, len=ln, flags=flags, kind="parse", desc=desc,
+                    algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame="IMIX")
+    if cfg == "nat64":
+        arena, off, ln = synth.nat64_stream(n, seed=seed)
+        desc = "1M x 256B IPv6/TCP -> IPv4 6to4 rewrite + TCP/IPv4 checksums (examples/nat64)"
+        return dict(arena=arena, off=off, len=ln, flags=0, kind="nat64", desc=desc,
+                    algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame="256B")
+    raise SystemExit(f"unknown config {cfg}")
+
+
+def imix_header_bytes_workload(seed):
+    """IMIX parse+hash: algorithmic bytes = headers touched + 6 B descriptor."""
+    from capsule_amd import _native as N
+    from capsule_amd import synth
+
+    n = 1 << 20
+    arena, off, ln = synth.imix(n, seed=seed)
+    eth = np.full(n, 14, np.int64)
+    l3 = np.zeros(n, np.int64)
+    l4 = np.zeros(n, np.int64)
+    # decode the synthetic frames' layer kinds from their bytes (host-side bookkeeping)
+    o = off.astype(np.int64)
+    et = arena[o + 12].astype(np.int64) * 256 + arena[o + 13]
+    v6 = et == 0x86DD
+    l3 = np.where(v6, 40, 20)
+    proto = np.where(v6, arena[o + 14 + 6], arena[o + 14 + 9])
+    l4 = np.where(proto == 17, 8, 20)
+    algo = int((eth + l3 + l4 + 6).sum())
+    flags = N.F_ACCEPT_ALL | N.F_FLOW_HASH
+    return dict(arena=arena, off=off, len=ln, flags=flags, kind="parse", frame="IMIX",
+                desc="1M IMIX 64/570/1500 7:4:1 v4/v6 x UDP/TCP: parse + 5-tuple hash",
+                algo_bytes=algo)
+
+
+def cpu_baseline(w, seconds):
+    """The C oracle (CPU restatement of the reference path, test infra) on
+    the same batch, one host core, time-bounded sample."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+
+    L = oracle_lib.lib()
+    arena, off, ln = w["arena"], w["off"], w["len"]
+    n = len(off)
+    p = lambda a: a.ctypes.data  # noqa: E731
+    if w["kind"] == "parse":
+        meta = np.zeros(n, np.uint32)
+        csum = np.zeros(n, np.uint32)
+        h = np.zeros(n, np.uint64)
+        run = lambda: L.or_parse_batch(p(arena), p(off), p(ln), n, w["flags"], p(meta),  # noqa
+                                       p(csum), p(h), None)
+    else:
+        pm = oracle_lib.PortMap()
+        out = np.zeros(len(arena), np.uint8)
+        olen = np.zeros(n, np.uint16)
+        disp = np.zeros(n, np.uint8)
+        st = np.zeros(n, np.uint8)
+        run = lambda: L.or_nat64_6to4(pm.h, p(arena), p(off), p(ln), n, p(out), p(off),  # noqa
+                                      p(olen), p(disp), p(st))
+    run()  # warm
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        run()
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    res = {"value": round(passes * n / el / 1e6, 3), "unit": "Mpps", "cores": 1,
+           "kind": "port",
+           "sample": f"C oracle (oracle/oracle.c) over the same {n}-packet batch, "
+                     f"{passes} passes, {el:.1f} s, 1 thread"}
+    if w["kind"] == "parse" and w["frame"] == "64B":
+        # the reference bench's own routine (bench/packets.rs:65-69 multi_parse_udp),
+        # batches of 500 like bench/packets.rs:31
+        passes, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < min(3.0, seconds):
+            for s in range(0, n, 500):
+                e = min(n, s + 500)
+                L.or_multi_parse_udp(p(arena), p(off[s:e]), p(ln[s:e]), e - s)
+            passes += 1
+        el = time.perf_counter() - t0
+        res["multi_parse_udp_mpps"] = round(passes * n / el / 1e6, 3)
+    try:
+        res["host_cpu"] = next(x.split(":", 1)[1].strip() for x in
+                               open("/proc/cpuinfo") if x.startswith("model name"))
+    except Exception:
+        pass
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--config", default="parse64",
+                    choices=["parse64", "imix", "imix_csum", "nat64"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    from capsule_amd import _native as N
+    from capsule_amd import packets
+    from capsule_amd.shards import ShardGroup
+
+    g = ShardGroup()
+    dev = torch.device("cuda", g.local_rank)
+    torch.cuda.set_device(dev)
+    seed = g.shard_seed(0xC0FFEE + {"parse64": 2, "imix": 3, "imix_csum": 3, "nat64": 4}[args.config])
+    w = make_workload(args.config, seed)
+    n = len(w["off"])
+    ctx = packets.Context(g.local_rank)
+
+    # R resident copies so the rotation's footprint exceeds the Infinity Cache
+    batch_bytes = len(w["arena"]) + 6 * n
+    copies = max(2, -(-2 * INFINITY_CACHE // batch_bytes))
+    b0 = packets.PacketBatch.from_numpy(w["arena"], w["off"], w["len"], dev)
+    batches = [b0] + [packets.PacketBatch(b0.arena.clone(), b0.off.clone(), b0.len.clone())
+                      for _ in range(copies - 1)]
+    stream = torch.cuda.current_stream(dev)
+
+    if w["kind"] == "parse":
+        outs = [packets.ParseBuffers(n, dev) for _ in range(2)]
+
+        def launch(k):
+            packets.parse(ctx, batches[k % copies], flags=w["flags"], out=outs[k & 1],
+                          stream=stream)
+    else:
+        gw = packets.Nat64Gateway(ctx, capacity_log2=17)
+        nat_out = [(torch.empty_like(b.arena), b.off, torch.empty(n, dtype=torch.int16, device=dev),
+                    torch.empty(n, dtype=torch.uint8, device=dev),
+                    torch.empty(n, dtype=torch.uint8, device=dev)) for b in batches[:2]]
+
+        def launch(k):
+            gw.nat_6to4(batches[k % copies], stream=stream, out=nat_out[k & 1])
+
+    for k in range(args.warmup):
+        launch(k)
+    torch.cuda.synchronize(dev)
+
+    step = [0]
+
+    def one():
+        launch(step[0])
+        step[0] += 1
+
+    elapsed = g.timed(one, args.steps, sync=lambda: torch.cuda.synchronize(dev))
+
+    # per-launch kernel time with HIP events on the launch stream (separate pass
+    # so the events do not perturb the timed region)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(min(args.steps, 200))]
+    for k, (a, b) in enumerate(ev):
+        a.record(stream)
+        launch(k)
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    achieved = w["algo_bytes"] / (kern_ms * 1e-3) / 1e9
+
+    total_pkts = g.sum(n * args.steps)
+    value = total_pkts / elapsed / 1e6
+    frac_all = g.sum(achieved / HBM_PEAK_GBS) / g.world
+    result = {
+        "metric": "Mpps device-resident parse+cksum+hash @64/256/1500B; % HBM-read roofline",
+        "value": round(value, 2),
+        "unit": "Mpps",
+        "n_gpus": g.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded proptest-style reconciled frames, one shard per rank)",
+        "config": {"workload": w["desc"], "config": args.config, "packets_per_step": n,
+                   "global_batch": n * g.world, "resident_copies": copies,
+                   "parallelism": f"{g.world} independent RX-queue shards (no collective)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "kernel_us": round(kern_ms * 1e3, 3),
+                     "algo_bytes_per_launch": w["algo_bytes"],
+                     "mean_frac_over_ranks": round(frac_all, 4)},
+    }
+    if g.world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
+    if g.rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    g.close()
+
+
+if __name__ == "__main__":
+    main()

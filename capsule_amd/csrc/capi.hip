@@ -1,0 +1,354 @@
+// capi.hip — the extern "C" boundary declared in include/capsule_gpu.h.
+//
+// Error handling follows the reference's FFI conventions
+// (core/src/ffi.rs:86-141, core/src/dpdk/mod.rs:62-70): every entry point
+// returns 0 or a negative errno-style code and records it in a thread-local
+// slot readable through cgpu_last_error(), the `_rte_errno()` analogue of
+// ffi/src/shim.c:24-26.  Contexts are independent (one per core thread /
+// RX queue) and no global lock is taken on the launch path.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <new>
+
+#include "capsule_gpu.h"
+#include "kernels.hpp"
+
+namespace {
+
+thread_local int g_last_error = 0;
+
+int fail(int code) {
+  g_last_error = code;
+  return code;
+}
+
+int ok() {
+  g_last_error = 0;
+  return 0;
+}
+
+int hip_fail(hipError_t e) {
+  (void)e;
+  return fail(CGPU_EIO);
+}
+
+}  // namespace
+
+struct cgpu_ctx {
+  int device;
+  hipStream_t stream;  // used by the synchronous host entry points
+  // pinned + device staging for cgpu_parse_host
+  uint8_t *h_arena = nullptr, *d_arena = nullptr;
+  size_t arena_cap = 0;
+  uint8_t *h_desc = nullptr, *d_desc = nullptr;  // off[n] | len[n] | outputs
+  size_t desc_cap = 0;
+};
+
+struct cgpu_portmap {
+  cgpu_ctx *ctx;
+  cgpu::PortMapDev dev;
+  void *mem;
+  // per-call scratch
+  uint32_t *pkt_slot = nullptr;
+  uint32_t *block_sums = nullptr;
+  uint32_t scratch_n = 0;
+};
+
+extern "C" {
+
+int cgpu_abi_version(void) { return CGPU_ABI_VERSION; }
+
+int cgpu_last_error(void) { return g_last_error; }
+
+const char *cgpu_strerror(int code) {
+  switch (code) {
+    case CGPU_OK: return "success";
+    case CGPU_EINVAL: return "invalid argument";
+    case CGPU_ENOMEM: return "out of memory";
+    case CGPU_ENODEV: return "no such device";
+    case CGPU_EIO: return "HIP runtime error";
+    case CGPU_ENOSPC: return "port table full";
+    default: return "unknown error";
+  }
+}
+
+const char *cgpu_pkt_status_str(int s) {
+  switch (s) {
+    case CGPU_PKT_OK: return "ok";
+    case CGPU_PKT_ETH_BAD_OFFSET: return "Ethernet: bad offset";
+    case CGPU_PKT_ETH_OUT_OF_BUFFER: return "Ethernet: out of buffer";
+    case CGPU_PKT_NOT_IPV4: return "not an IPv4 packet.";
+    case CGPU_PKT_NOT_IPV6: return "not an IPv6 packet.";
+    case CGPU_PKT_NOT_IP: return "not an IP packet.";
+    case CGPU_PKT_L3_BAD_OFFSET: return "IP: bad offset";
+    case CGPU_PKT_L3_OUT_OF_BUFFER: return "IP: out of buffer";
+    case CGPU_PKT_NOT_UDP: return "not a UDP packet.";
+    case CGPU_PKT_NOT_TCP: return "not a TCP packet.";
+    case CGPU_PKT_NOT_L4: return "not a UDP or TCP packet.";
+    case CGPU_PKT_L4_BAD_OFFSET: return "L4: bad offset";
+    case CGPU_PKT_L4_OUT_OF_BUFFER: return "L4: out of buffer";
+    case CGPU_PKT_NOT_RESIZED: return "buffer not resized";
+    case CGPU_PKT_TABLE_FULL: return "port table full";
+    default: return "unknown status";
+  }
+}
+
+int cgpu_ctx_create(int hip_device, cgpu_ctx **out) {
+  if (!out) return fail(CGPU_EINVAL);
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || hip_device < 0 || hip_device >= count)
+    return fail(CGPU_ENODEV);
+  if (hipSetDevice(hip_device) != hipSuccess) return fail(CGPU_ENODEV);
+  cgpu_ctx *c = new (std::nothrow) cgpu_ctx();
+  if (!c) return fail(CGPU_ENOMEM);
+  c->device = hip_device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return fail(CGPU_EIO);
+  }
+  *out = c;
+  return ok();
+}
+
+void cgpu_ctx_destroy(cgpu_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->h_arena) (void)hipHostFree(c->h_arena);
+  if (c->d_arena) (void)hipFree(c->d_arena);
+  if (c->h_desc) (void)hipHostFree(c->h_desc);
+  if (c->d_desc) (void)hipFree(c->d_desc);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+static int check_batch(const cgpu_batch *b) {
+  if (!b) return CGPU_EINVAL;
+  if (b->n == 0) return 0;
+  if (!b->arena || !b->off || !b->len) return CGPU_EINVAL;
+  if (b->arena_len >= (1ull << 32)) return CGPU_EINVAL;
+  return 0;
+}
+
+int cgpu_parse_batch(cgpu_ctx *ctx, const cgpu_batch *batch, uint32_t flags,
+                     const cgpu_parse_out *out, void *stream) {
+  if (!ctx || !out) return fail(CGPU_EINVAL);
+  if (int e = check_batch(batch)) return fail(e);
+  if (batch->n == 0) return ok();
+  if (!out->meta) return fail(CGPU_EINVAL);
+  if ((flags & (CGPU_F_CSUM_IP | CGPU_F_CSUM_L4)) && !out->csum) return fail(CGPU_EINVAL);
+  if ((flags & CGPU_F_FLOW_HASH) && !out->flow_hash) return fail(CGPU_EINVAL);
+  if ((flags & CGPU_F_ACCEPT_ALL) == 0) flags |= CGPU_F_ACCEPT_ALL;
+  cgpu::ParseArgs a;
+  a.arena = batch->arena;
+  a.arena_len = (uint32_t)batch->arena_len;
+  a.off = batch->off;
+  a.len = batch->len;
+  a.n = batch->n;
+  a.accept = flags & CGPU_F_ACCEPT_ALL;
+  a.meta = out->meta;
+  a.csum = out->csum;
+  a.hash = out->flow_hash;
+  a.fields = out->fields;
+  hipError_t e = cgpu::launch_parse(a, flags, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e);
+  return ok();
+}
+
+static int grow(uint8_t **h, uint8_t **d, size_t *cap, size_t need) {
+  if (need <= *cap) return 0;
+  size_t nc = need + need / 2 + 4096;
+  if (*h) (void)hipHostFree(*h);
+  if (*d) (void)hipFree(*d);
+  *h = nullptr;
+  *d = nullptr;
+  *cap = 0;
+  if (hipHostMalloc((void **)h, nc, hipHostMallocDefault) != hipSuccess) return CGPU_ENOMEM;
+  if (hipMalloc((void **)d, nc) != hipSuccess) {
+    (void)hipHostFree(*h);
+    *h = nullptr;
+    return CGPU_ENOMEM;
+  }
+  *cap = nc;
+  return 0;
+}
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int cgpu_parse_host(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *len, uint32_t n,
+                    uint32_t flags, uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
+                    cgpu_hdr_record *fields) {
+  if (!ctx) return fail(CGPU_EINVAL);
+  if (n == 0) return ok();
+  if (!pkt || !len || !meta) return fail(CGPU_EINVAL);
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
+  // Gather into pinned staging at 64-byte slots (the mbuf data room layout).
+  size_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!pkt[i] && len[i]) return fail(CGPU_EINVAL);
+    total += align_up(len[i], 64);
+  }
+  if (total >= (1ull << 32)) return fail(CGPU_EINVAL);
+  if (int e = grow(&ctx->h_arena, &ctx->d_arena, &ctx->arena_cap, total + 64)) return fail(e);
+  const size_t o_off = 0, o_len = align_up(4ull * n, 256), o_meta = o_len + align_up(2ull * n, 256);
+  const size_t o_csum = o_meta + align_up(4ull * n, 256), o_hash = o_csum + align_up(4ull * n, 256);
+  const size_t o_fields = o_hash + align_up(8ull * n, 256);
+  const size_t dbytes = o_fields + (fields ? sizeof(cgpu_hdr_record) * (size_t)n : 0);
+  if (int e = grow(&ctx->h_desc, &ctx->d_desc, &ctx->desc_cap, dbytes)) return fail(e);
+  uint32_t *hoff = (uint32_t *)(ctx->h_desc + o_off);
+  uint16_t *hlen = (uint16_t *)(ctx->h_desc + o_len);
+  size_t pos = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    hoff[i] = (uint32_t)pos;
+    hlen[i] = len[i];
+    if (len[i]) memcpy(ctx->h_arena + pos, pkt[i], len[i]);
+    pos += align_up(len[i], 64);
+  }
+  hipStream_t s = ctx->stream;
+  if (hipMemcpyAsync(ctx->d_arena, ctx->h_arena, pos ? pos : 1, hipMemcpyHostToDevice, s) !=
+      hipSuccess)
+    return fail(CGPU_EIO);
+  if (hipMemcpyAsync(ctx->d_desc, ctx->h_desc, o_meta, hipMemcpyHostToDevice, s) != hipSuccess)
+    return fail(CGPU_EIO);
+  cgpu_batch b;
+  b.arena = ctx->d_arena;
+  b.arena_len = pos ? pos : 1;
+  b.off = (const uint32_t *)(ctx->d_desc + o_off);
+  b.len = (const uint16_t *)(ctx->d_desc + o_len);
+  b.n = n;
+  cgpu_parse_out o;
+  o.meta = (uint32_t *)(ctx->d_desc + o_meta);
+  o.csum = (uint32_t *)(ctx->d_desc + o_csum);
+  o.flow_hash = (uint64_t *)(ctx->d_desc + o_hash);
+  o.fields = fields ? (cgpu_hdr_record *)(ctx->d_desc + o_fields) : nullptr;
+  if (!csum) flags &= ~(CGPU_F_CSUM_IP | CGPU_F_CSUM_L4);
+  if (!flow_hash) flags &= ~CGPU_F_FLOW_HASH;
+  if (int e = cgpu_parse_batch(ctx, &b, flags, &o, s)) return e;
+  if (hipMemcpyAsync(meta, o.meta, 4ull * n, hipMemcpyDeviceToHost, s) != hipSuccess)
+    return fail(CGPU_EIO);
+  if (csum && hipMemcpyAsync(csum, o.csum, 4ull * n, hipMemcpyDeviceToHost, s) != hipSuccess)
+    return fail(CGPU_EIO);
+  if (flow_hash &&
+      hipMemcpyAsync(flow_hash, o.flow_hash, 8ull * n, hipMemcpyDeviceToHost, s) != hipSuccess)
+    return fail(CGPU_EIO);
+  if (fields && hipMemcpyAsync(fields, o.fields, sizeof(cgpu_hdr_record) * (size_t)n,
+                               hipMemcpyDeviceToHost, s) != hipSuccess)
+    return fail(CGPU_EIO);
+  if (hipStreamSynchronize(s) != hipSuccess) return fail(CGPU_EIO);
+  return ok();
+}
+
+int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_port,
+                        cgpu_portmap **out) {
+  if (!ctx || !out || capacity_log2 < 4 || capacity_log2 > 30) return fail(CGPU_EINVAL);
+  *out = nullptr;
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
+  const size_t cap = (size_t)1 << capacity_log2;
+  const size_t bytes = cap * 4 * (1 + 1 + 4 + 1 + 1) + 256;
+  void *mem = nullptr;
+  if (hipMalloc(&mem, bytes) != hipSuccess) return fail(CGPU_ENOMEM);
+  cgpu_portmap *pm = new (std::nothrow) cgpu_portmap();
+  if (!pm) {
+    (void)hipFree(mem);
+    return fail(CGPU_ENOMEM);
+  }
+  pm->ctx = ctx;
+  pm->mem = mem;
+  uint32_t *p = (uint32_t *)mem;
+  pm->dev.state = p;
+  p += 64;
+  pm->dev.slot_ref = p;
+  p += cap;
+  pm->dev.slot_min = p;
+  p += cap;
+  pm->dev.key_src = p;
+  p += 4 * cap;
+  pm->dev.key_port = p;
+  p += cap;
+  pm->dev.slot_port = p;
+  pm->dev.cap_mask = (uint32_t)(cap - 1);
+  if (cgpu::launch_portmap_init(pm->dev, first_port, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    (void)hipFree(mem);
+    delete pm;
+    return fail(CGPU_EIO);
+  }
+  *out = pm;
+  return ok();
+}
+
+void cgpu_portmap_destroy(cgpu_portmap *pm) {
+  if (!pm) return;
+  (void)hipSetDevice(pm->ctx->device);
+  (void)hipDeviceSynchronize();
+  if (pm->pkt_slot) (void)hipFree(pm->pkt_slot);
+  (void)hipFree(pm->mem);
+  delete pm;
+}
+
+static int read_state(cgpu_portmap *pm, uint32_t st[4]) {
+  if (hipSetDevice(pm->ctx->device) != hipSuccess) return CGPU_ENODEV;
+  if (hipDeviceSynchronize() != hipSuccess) return CGPU_EIO;
+  if (hipMemcpy(st, pm->dev.state, 16, hipMemcpyDeviceToHost) != hipSuccess) return CGPU_EIO;
+  return 0;
+}
+
+int cgpu_portmap_next_port(cgpu_portmap *pm, uint16_t *next_port) {
+  if (!pm || !next_port) return fail(CGPU_EINVAL);
+  uint32_t st[4];
+  if (int e = read_state(pm, st)) return fail(e);
+  *next_port = (uint16_t)st[0];
+  return ok();
+}
+
+int cgpu_portmap_size(cgpu_portmap *pm, uint32_t *entries) {
+  if (!pm || !entries) return fail(CGPU_EINVAL);
+  uint32_t st[4];
+  if (int e = read_state(pm, st)) return fail(e);
+  *entries = st[1];
+  return ok();
+}
+
+int cgpu_nat64_6to4(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8_t *out_arena,
+                    uint64_t out_arena_len, const uint32_t *out_off, uint16_t *out_len,
+                    uint8_t *disposition, uint8_t *status, void *stream) {
+  if (!ctx || !pm) return fail(CGPU_EINVAL);
+  if (int e = check_batch(in)) return fail(e);
+  if (in->n == 0) return ok();
+  if (!out_arena || !out_off || !out_len || !disposition || !status) return fail(CGPU_EINVAL);
+  if (out_arena_len >= (1ull << 32)) return fail(CGPU_EINVAL);
+  if (in->n >= 0x7fffffffu) return fail(CGPU_EINVAL);
+  if (pm->scratch_n < in->n) {
+    if (pm->pkt_slot) (void)hipFree(pm->pkt_slot);
+    pm->pkt_slot = nullptr;
+    pm->scratch_n = 0;
+    const size_t nb = cgpu::nat64_num_blocks(in->n) + 1;
+    void *m = nullptr;
+    if (hipMalloc(&m, 4ull * in->n + 4ull * nb + 256) != hipSuccess) return fail(CGPU_ENOMEM);
+    pm->pkt_slot = (uint32_t *)m;
+    pm->block_sums = (uint32_t *)((uint8_t *)m + align_up(4ull * in->n, 256));
+    pm->scratch_n = in->n;
+  }
+  cgpu::Nat64Args a;
+  a.arena = in->arena;
+  a.arena_len = (uint32_t)in->arena_len;
+  a.off = in->off;
+  a.len = in->len;
+  a.n = in->n;
+  a.out_arena = out_arena;
+  a.out_arena_len = (uint32_t)out_arena_len;
+  a.out_off = out_off;
+  a.out_len = out_len;
+  a.disposition = disposition;
+  a.status = status;
+  a.pkt_slot = pm->pkt_slot;
+  a.block_sums = pm->block_sums;
+  a.pm = pm->dev;
+  hipError_t e = cgpu::launch_nat64_6to4(a, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e);
+  return ok();
+}
+
+}  // extern "C"

@@ -1,0 +1,273 @@
+"""Host-side mirror of the reference's packet API for the GPU hot path.
+
+The reference processes one `Mbuf` at a time through typed parses
+(`packet.parse::<Ethernet>()?.parse::<Ipv4>()?.parse::<Udp4>()?`,
+core/src/packets/mod.rs:178) inside batch combinators (core/src/batch/).
+Here the unit is a *burst*: a `PacketBatch` is the device image of many
+single-segment mbufs (an arena of frame bytes plus per-packet offset and
+data_len, core/src/dpdk/mbuf.rs:196-205), and one call runs the whole chain
+for every packet on the GPU.  Per-packet `Result`s become a status code per
+packet carrying the same distinctions as the reference's errors
+(`BufferError::{BadOffset, OutOfBuffer}` mbuf.rs:85-98, "not an IPv4
+packet." v4.rs:430, ...), see `ParsedBatch.error()`.
+
+Device memory and streams come from torch (plumbing only); every byte of
+packet work runs in the HIP kernels behind include/capsule_gpu.h.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+_STATUS_MSG = {
+    N.PKT["ETH_BAD_OFFSET"]: "BadOffset",
+    N.PKT["ETH_OUT_OF_BUFFER"]: "OutOfBuffer",
+    N.PKT["L3_BAD_OFFSET"]: "BadOffset",
+    N.PKT["L3_OUT_OF_BUFFER"]: "OutOfBuffer",
+    N.PKT["L4_BAD_OFFSET"]: "BadOffset",
+    N.PKT["L4_OUT_OF_BUFFER"]: "OutOfBuffer",
+}
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream_handle(stream):
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+class Context:
+    """`cgpu_ctx`: one per core thread / RX queue (runtime/core_map.rs:236-293)."""
+
+    def __init__(self, device=0):
+        if not torch.cuda.is_available():
+            raise RuntimeError("capsule_amd: no HIP device visible")
+        self.device = torch.device("cuda", device)
+        self._h = ctypes.c_void_p()
+        N.check(N.lib().cgpu_ctx_create(device, ctypes.byref(self._h)), "cgpu_ctx_create")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            N.lib().cgpu_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PacketBatch:
+    """Device image of a burst of mbufs: arena (u8), off (u32), len (u16)."""
+
+    def __init__(self, arena, off, length):
+        assert arena.dtype == torch.uint8 and off.dtype == torch.int32
+        assert length.dtype == torch.int16 and off.numel() == length.numel()
+        self.arena, self.off, self.len = arena, off, length
+
+    @property
+    def n(self):
+        return self.off.numel()
+
+    @classmethod
+    def from_numpy(cls, arena, off, length, device):
+        """Copy a host batch (np.uint8 arena, np.uint32 off, np.uint16 len)."""
+        a = torch.from_numpy(np.ascontiguousarray(arena, dtype=np.uint8)).to(device)
+        o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint32).view(np.int32)).to(device)
+        ln = torch.from_numpy(np.ascontiguousarray(length, dtype=np.uint16).view(np.int16)).to(device)
+        return cls(a, o, ln)
+
+    @classmethod
+    def from_frames(cls, frames, device, slot=64):
+        """Pack a list of byte strings at `slot`-aligned offsets."""
+        from .synth import pack_frames
+
+        return cls.from_numpy(*pack_frames(frames, slot), device)
+
+    def cbatch(self):
+        b = N.Batch()
+        b.arena = self.arena.data_ptr()
+        b.arena_len = self.arena.numel()
+        b.off = self.off.data_ptr()
+        b.len = self.len.data_ptr()
+        b.n = self.n
+        return b
+
+    def frame(self, i):
+        o = int(self.off[i].item()) & 0xFFFFFFFF
+        ln = int(self.len[i].item()) & 0xFFFF
+        return bytes(self.arena[o : o + ln].cpu().numpy())
+
+
+class ParsedBatch:
+    """SoA result of `parse`: meta, csum, flow_hash, fields (device tensors)."""
+
+    def __init__(self, meta, csum, flow_hash, fields):
+        self.meta, self.csum, self.flow_hash, self.fields = meta, csum, flow_hash, fields
+
+    def status(self):
+        return self.meta & 0xFF
+
+    def ok(self):
+        return self.status() == 0
+
+    def ip_csum(self):
+        return self.csum & 0xFFFF
+
+    def l4_csum(self):
+        return (self.csum >> 16) & 0xFFFF
+
+    def error(self, i):
+        """Reference error text of packet i (None when every layer parsed)."""
+        s = int(self.meta[i].item()) & 0xFF
+        if s == 0:
+            return None
+        msg = N.lib().cgpu_pkt_status_str(s).decode()
+        return _STATUS_MSG.get(s, msg) if s in _STATUS_MSG else msg
+
+    def fields_numpy(self):
+        if self.fields is None:
+            return None
+        raw = self.fields.cpu().numpy()
+        return raw.view(np.dtype(N.HDR_RECORD_FIELDS)).reshape(-1)
+
+
+def parse_flags(accept=N.F_ACCEPT_ALL, csum_ip=True, csum_l4=True, flow_hash=True):
+    f = accept
+    if csum_ip:
+        f |= N.F_CSUM_IP
+    if csum_l4:
+        f |= N.F_CSUM_L4
+    if flow_hash:
+        f |= N.F_FLOW_HASH
+    return f
+
+
+class ParseBuffers:
+    """Preallocated outputs for repeated `parse` calls on same-sized bursts."""
+
+    def __init__(self, n, device, fields=False):
+        self.meta = torch.empty(n, dtype=torch.int32, device=device)
+        self.csum = torch.empty(n, dtype=torch.int32, device=device)
+        self.flow_hash = torch.empty(n, dtype=torch.int64, device=device)
+        self.fields = (torch.empty((n, N.HDR_RECORD_SIZE), dtype=torch.uint8, device=device)
+                       if fields else None)
+
+
+def parse(ctx, batch, flags=None, fields=False, out=None, stream=None):
+    """Batched Ethernet -> Ipv4/Ipv6 -> Udp/Tcp parse + checksums + flow hash.
+
+    Mirrors `parse::<Ethernet>()` (ethernet.rs:279) -> `parse::<Ipv4|Ipv6>()`
+    (v4.rs:427, v6/mod.rs:274) -> `parse::<Udp|Tcp>()` (udp.rs:287, tcp.rs:558),
+    plus `compute_checksum` evaluated on the bytes as they are and the hash of
+    `flow()`.  Asynchronous on `stream` (torch's current stream by default).
+    """
+    if flags is None:
+        flags = parse_flags()
+    n = batch.n
+    if out is None:
+        out = ParseBuffers(n, batch.arena.device, fields)
+    po = N.ParseOut()
+    po.meta = out.meta.data_ptr()
+    po.csum = out.csum.data_ptr()
+    po.flow_hash = out.flow_hash.data_ptr()
+    po.fields = out.fields.data_ptr() if (fields and out.fields is not None) else None
+    cb = batch.cbatch()
+    rc = N.lib().cgpu_parse_batch(ctx.handle, ctypes.byref(cb), flags, ctypes.byref(po),
+                                  _stream_handle(stream))
+    N.check(rc, "cgpu_parse_batch")
+    return ParsedBatch(out.meta[:n], out.csum[:n], out.flow_hash[:n],
+                       out.fields[:n] if (fields and out.fields is not None) else None)
+
+
+def parse_host(ctx, frames, flags=None, fields=False):
+    """Host-memory variant (the DPDK seam): frames is a list of bytes."""
+    if flags is None:
+        flags = parse_flags()
+    n = len(frames)
+    bufs = [ctypes.create_string_buffer(bytes(f), max(1, len(f))) for f in frames]
+    ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(b, ctypes.c_void_p).value for b in bufs])
+    lens = np.array([len(f) for f in frames], dtype=np.uint16)
+    meta = np.zeros(n, np.uint32)
+    csum = np.zeros(n, np.uint32)
+    fh = np.zeros(n, np.uint64)
+    fl = np.zeros((n, N.HDR_RECORD_SIZE), np.uint8) if fields else None
+    rc = N.lib().cgpu_parse_host(
+        ctx.handle, ptrs, lens.ctypes.data, n, flags, meta.ctypes.data, csum.ctypes.data,
+        fh.ctypes.data, fl.ctypes.data if fields else None)
+    N.check(rc, "cgpu_parse_host")
+    recs = fl.view(np.dtype(N.HDR_RECORD_FIELDS)).reshape(-1) if fields else None
+    return meta, csum, fh, recs
+
+
+class Nat64Gateway:
+    """examples/nat64 6to4 direction with its PORT_MAP on the device.
+
+    `NEXT_PORT` starts at `first_port` (1025 in examples/nat64/main.rs:42) and
+    wraps modulo 2^16 like `AtomicU16::fetch_add`.  Packets are assigned
+    gateway ports in batch order, so a stream cut into consecutive batches
+    gets exactly the ports the reference's single-core pipeline would.
+    """
+
+    def __init__(self, ctx, capacity_log2=20, first_port=1025):
+        self.ctx = ctx
+        self._h = ctypes.c_void_p()
+        N.check(N.lib().cgpu_portmap_create(ctx.handle, capacity_log2, first_port,
+                                            ctypes.byref(self._h)), "cgpu_portmap_create")
+
+    def next_port(self):
+        v = ctypes.c_uint16()
+        N.check(N.lib().cgpu_portmap_next_port(self._h, ctypes.byref(v)), "next_port")
+        return v.value
+
+    def size(self):
+        v = ctypes.c_uint32()
+        N.check(N.lib().cgpu_portmap_size(self._h, ctypes.byref(v)), "size")
+        return v.value
+
+    def nat_6to4(self, batch, out_arena=None, out_off=None, stream=None, out=None):
+        """Returns (out PacketBatch, disposition u8, status u8) on the device.
+
+        Output frame i is written at out_off[i] (default: in place of its
+        input slot in a fresh arena of the same size); out_len[i] is the new
+        data_len for ACT packets and 0 otherwise.
+        """
+        n = batch.n
+        dev = batch.arena.device
+        if out is None:
+            if out_arena is None:
+                out_arena = torch.zeros_like(batch.arena)
+            if out_off is None:
+                out_off = batch.off
+            out_len = torch.zeros(n, dtype=torch.int16, device=dev)
+            disp = torch.empty(n, dtype=torch.uint8, device=dev)
+            status = torch.empty(n, dtype=torch.uint8, device=dev)
+        else:
+            out_arena, out_off, out_len, disp, status = out
+        cb = batch.cbatch()
+        rc = N.lib().cgpu_nat64_6to4(
+            self.ctx.handle, self._h, ctypes.byref(cb), _ptr(out_arena), out_arena.numel(),
+            _ptr(out_off), _ptr(out_len), _ptr(disp), _ptr(status), _stream_handle(stream))
+        N.check(rc, "cgpu_nat64_6to4")
+        return PacketBatch(out_arena, out_off, out_len), disp, status
+
+    def close(self):
+        if self._h:
+            N.lib().cgpu_portmap_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

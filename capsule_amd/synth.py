@@ -1,0 +1,277 @@
+"""Seeded synthetic packet batches (host side, numpy).
+
+Mirrors the reference's proptest packet strategies
+(core/src/testils/proptest/strategy.rs:209-400): every settable header field
+is uniform random (`any::<T>()`), ether_type / protocol are implied by the
+layer stack, and the packet is `reconcile_all()`-ed, i.e. length fields and
+checksums are consistent (strategy.rs:395-397).  The reference's bench draws
+from proptest's deterministic RNG (testils/rvg.rs:40-44), which is not
+reproducible outside Rust, so batches here come from numpy's PCG64 with a
+fixed seed per configuration.
+
+A batch is (arena u8[], off u32[n], len u16[n]): packets sit at 64-byte
+aligned slots of a contiguous arena, the device image of a burst of mbufs.
+"""
+import numpy as np
+
+ETH_IPV4, ETH_IPV6 = 0x0800, 0x86DD
+UDP, TCP = 17, 6
+
+# kinds: (l3, l4) with l3 in {4, 6}, l4 in {UDP, TCP}
+V4_UDP, V4_TCP, V6_UDP, V6_TCP = (4, UDP), (4, TCP), (6, UDP), (6, TCP)
+
+
+def _fold(s):
+    s = s.astype(np.uint64)
+    while True:
+        hi = s >> np.uint64(16)
+        if not hi.any():
+            return s
+        s = (s & np.uint64(0xFFFF)) + hi
+
+
+def _be_word_sum(block):
+    """Sum of big-endian u16 words of each row (odd tail padded with 0)."""
+    m, L = block.shape
+    if L % 2:
+        block = np.concatenate([block, np.zeros((m, 1), np.uint8)], axis=1)
+    w = block.reshape(m, -1, 2).astype(np.uint64)
+    return (w[:, :, 0] * np.uint64(256) + w[:, :, 1]).sum(axis=1)
+
+
+def _put16(a, col, v):
+    v = np.asarray(v, dtype=np.uint64)
+    a[:, col] = (v >> np.uint64(8)).astype(np.uint8)
+    a[:, col + 1] = (v & np.uint64(0xFF)).astype(np.uint8)
+
+
+def _get16(a, col):
+    return a[:, col].astype(np.uint64) * np.uint64(256) + a[:, col + 1]
+
+
+def build_frames(rng, m, kind, frame_len, vlan=0, hop_limit_min=0):
+    """m reconciled frames of one kind and length, as an [m, frame_len] array.
+
+    vlan: 0 none, 1 802.1Q, 2 802.1ad (QinQ) tags (ethernet.rs:164-192).
+    """
+    l3, l4 = kind
+    eth_len = 14 + 4 * vlan
+    l3_len = 20 if l3 == 4 else 40
+    l4_len = 8 if l4 == UDP else 20
+    assert frame_len >= eth_len + l3_len + l4_len, (kind, frame_len)
+    f = rng.integers(0, 256, size=(m, frame_len), dtype=np.uint8)  # random payload
+    # Ethernet (strategy.rs:209-218): random dst/src MACs, ether_type implied.
+    et = ETH_IPV4 if l3 == 4 else ETH_IPV6
+    if vlan == 0:
+        _put16(f, 12, et)
+    elif vlan == 1:
+        _put16(f, 12, 0x8100)
+        _put16(f, 16, et)
+    else:
+        _put16(f, 12, 0x88A8)
+        _put16(f, 16, 0x8100)
+        _put16(f, 20, et)
+    o = eth_len
+    if l3 == 4:  # strategy.rs:220-260, pushed header defaults v4.rs:594-609
+        f[:, o] = 0x45
+        dscp = rng.integers(0, 256, m, dtype=np.uint16)
+        ecn = rng.integers(0, 256, m, dtype=np.uint16)
+        f[:, o + 1] = (((dscp << 2) & 0xFC) | (ecn & 0x03)).astype(np.uint8)
+        df = rng.integers(0, 2, m, dtype=np.uint16) * 0x4000
+        mf = rng.integers(0, 2, m, dtype=np.uint16) * 0x2000
+        frag = rng.integers(0, 65536, m, dtype=np.uint32) & 0x1FFF
+        _put16(f, o + 6, (df | mf | frag).astype(np.uint64))
+        f[:, o + 9] = l4
+        _put16(f, o + 2, frame_len - o)  # reconcile: total_length (v4.rs:486-489)
+    else:  # ip/v6/mod.rs setters; version 6, random dscp/ecn/flow label
+        w = (np.uint64(6) << np.uint64(28)) | rng.integers(0, 1 << 28, m, dtype=np.uint64)
+        for b in range(4):
+            f[:, o + b] = ((w >> np.uint64(24 - 8 * b)) & np.uint64(0xFF)).astype(np.uint8)
+        _put16(f, o + 4, frame_len - o - 40)  # reconcile: payload_length (v6 :331-334)
+        f[:, o + 6] = l4
+        if hop_limit_min:
+            f[:, o + 7] = rng.integers(hop_limit_min, 256, m, dtype=np.uint16).astype(np.uint8)
+    t = o + l3_len
+    if l4 == UDP:
+        _put16(f, t + 4, frame_len - t)  # reconcile: length (udp.rs:350-354)
+        cs_at = t + 6
+    else:
+        cs_at = t + 16
+    # L4 checksum over [t, frame_len) with the pseudo-header (checksum.rs).
+    _put16(f, cs_at, 0)
+    span = frame_len - t
+    if l3 == 4:
+        ph = _be_word_sum(f[:, o + 12 : o + 20]) + np.uint64(l4 + span)
+    else:
+        ph = _be_word_sum(f[:, o + 8 : o + 40]) + np.uint64(l4 + span)
+    s = _fold(_fold(ph) + _be_word_sum(f[:, t:]))
+    c = (~s) & np.uint64(0xFFFF)
+    if l4 == UDP:
+        c = np.where(c == 0, np.uint64(0xFFFF), c)  # udp.rs:137-140
+    _put16(f, cs_at, c)
+    if l3 == 4:  # header checksum last (reconcile_all order: L4 -> L3)
+        _put16(f, o + 10, 0)
+        _put16(f, o + 10, (~_fold(_be_word_sum(f[:, o : o + 20]))) & np.uint64(0xFFFF))
+    return f
+
+
+def place(groups, order, slot=64):
+    """Lay out frames of several same-length groups in `order` into an arena.
+
+    groups: list of [m_g, L_g] arrays; order: array of (group, row) pairs.
+    Returns (arena, off, len).
+    """
+    lens = np.array([groups[g].shape[1] for g, _ in order], dtype=np.uint64)
+    slots = (lens + np.uint64(slot - 1)) // np.uint64(slot) * np.uint64(slot)
+    off = np.zeros(len(order), dtype=np.uint64)
+    if len(order):
+        off[1:] = np.cumsum(slots)[:-1]
+    total = int(slots.sum()) if len(order) else 0
+    assert total < (1 << 32), "arena must stay below 4 GiB (u32 offsets)"
+    arena = np.zeros(max(total, slot), dtype=np.uint8)
+    order = np.asarray(order)
+    for g, arr in enumerate(groups):
+        idx = np.nonzero(order[:, 0] == g)[0] if len(order) else np.zeros(0, np.int64)
+        if not len(idx):
+            continue
+        L = arr.shape[1]
+        rows = order[idx, 1]
+        dst = (off[idx][:, None] + np.arange(L, dtype=np.uint64)[None, :]).astype(np.int64)
+        arena[dst.reshape(-1)] = arr[rows].reshape(-1)
+    return arena, off.astype(np.uint32), lens.astype(np.uint16)
+
+
+def uniform(n, kind=V4_UDP, frame_len=64, seed=0xC0FFEE, vlan=0, slot=64, hop_limit_min=0):
+    """n frames of one kind and size (BASELINE configs 2 and 4)."""
+    rng = np.random.default_rng(seed)
+    f = build_frames(rng, n, kind, frame_len, vlan, hop_limit_min)
+    if slot == frame_len:  # contiguous: no scatter needed
+        return f.reshape(-1).copy(), (np.arange(n, dtype=np.uint64) * frame_len).astype(
+            np.uint32), np.full(n, frame_len, np.uint16)
+    order = np.stack([np.zeros(n, np.int64), np.arange(n)], axis=1)
+    return place([f], order, slot)
+
+
+IMIX_SIZES = (64, 570, 1500)
+IMIX_WEIGHTS = (7, 4, 1)
+
+
+def imix(n, seed=0xC0FFEE + 3, v6_frac=0.5, tcp_frac=0.5, vlan_frac=0.0, slot=64):
+    """IMIX 64/570/1500 B at 7:4:1, mixed v4/v6 x UDP/TCP, shuffled (config 3).
+
+    64-B frames cannot hold IPv6/TCP (74 B minimum), so 64-B slots draw from
+    {v4/UDP, v4/TCP, v6/UDP}.
+    """
+    rng = np.random.default_rng(seed)
+    w = np.array(IMIX_WEIGHTS, dtype=np.float64)
+    size_idx = rng.choice(len(IMIX_SIZES), size=n, p=w / w.sum())
+    is6 = rng.random(n) < v6_frac
+    istcp = rng.random(n) < tcp_frac
+    small = size_idx == 0
+    istcp = np.where(small & is6, False, istcp)
+    vl = np.where(rng.random(n) < vlan_frac, rng.integers(1, 3, n), 0)
+    vl = np.where(small & is6, 0, vl)  # 64-B v6/UDP has no room for a tag
+    groups, order_g, order_r = [], np.zeros(n, np.int64), np.zeros(n, np.int64)
+    for si, size in enumerate(IMIX_SIZES):
+        for l3 in (4, 6):
+            for l4 in (UDP, TCP):
+                for v in (0, 1, 2):
+                    sel = np.nonzero((size_idx == si) & (is6 == (l3 == 6)) &
+                                     (istcp == (l4 == TCP)) & (vl == v))[0]
+                    if not len(sel):
+                        continue
+                    groups.append(build_frames(rng, len(sel), (l3, l4), size, v))
+                    order_g[sel] = len(groups) - 1
+                    order_r[sel] = np.arange(len(sel))
+    return place(groups, np.stack([order_g, order_r], axis=1), slot)
+
+
+def nat64_stream(n, frame_len=256, n_keys=50_000, seed=0xC0FFEE + 4, slot=None,
+                 drop_frac=0.0):
+    """IPv6/TCP frames for the 6to4 rewrite (config 4).
+
+    Sources come from a pool of `n_keys` distinct (v6 src, tcp src port)
+    keys so that NEXT_PORT never wraps for n_keys < 64511; hop_limit is in
+    [1, 255] (hop_limit 0 panics in a Rust debug build).  `drop_frac` of the
+    packets are IPv6/UDP, which nat_6to4 drops (main.rs:124, 148).
+    """
+    rng = np.random.default_rng(seed)
+    f = build_frames(rng, n, V6_TCP, frame_len, 0, hop_limit_min=1)
+    key_src = rng.integers(0, 256, size=(n_keys, 16), dtype=np.uint8)
+    key_port = rng.integers(0, 65536, size=n_keys, dtype=np.uint64)
+    pick = rng.integers(0, n_keys, size=n)
+    f[:, 22:38] = key_src[pick]
+    _put16(f, 54, key_port[pick])
+    if drop_frac:
+        f[rng.random(n) < drop_frac, 20] = UDP
+    # re-reconcile the TCP checksum after changing src / port
+    o, t = 14, 54
+    _put16(f, t + 16, 0)
+    span = frame_len - t
+    ph = _be_word_sum(f[:, o + 8 : o + 40]) + np.uint64(TCP + span)
+    s = _fold(_fold(ph) + _be_word_sum(f[:, t:]))
+    _put16(f, t + 16, (~s) & np.uint64(0xFFFF))
+    slot = slot or frame_len
+    if slot == frame_len:
+        return f.reshape(-1).copy(), (np.arange(n, dtype=np.uint64) * frame_len).astype(
+            np.uint32), np.full(n, frame_len, np.uint16)
+    return place([f], np.stack([np.zeros(n, np.int64), np.arange(n)], axis=1), slot)
+
+
+def pack_frames(frames, slot=64):
+    """Pack arbitrary byte strings at `slot`-aligned offsets."""
+    lens = np.array([len(f) for f in frames], dtype=np.uint64)
+    slots = np.maximum((lens + np.uint64(slot - 1)) // np.uint64(slot), 1) * np.uint64(slot)
+    off = np.zeros(len(frames), np.uint64)
+    if len(frames):
+        off[1:] = np.cumsum(slots)[:-1]
+    arena = np.zeros(max(int(slots.sum()), slot), np.uint8)
+    for i, fr in enumerate(frames):
+        arena[int(off[i]) : int(off[i]) + len(fr)] = np.frombuffer(bytes(fr), np.uint8)
+    return arena, off.astype(np.uint32), lens.astype(np.uint16)
+
+
+def fuzz(n, seed=1, max_len=1600):
+    """Edge-case batch: every kind, VLAN depth, truncations, wrong ether_types
+    and protocols, odd lengths and UNALIGNED arena offsets (any byte).
+
+    Returns (arena, off, len) with packets at random byte offsets.
+    """
+    rng = np.random.default_rng(seed)
+    frames = []
+    kinds = [V4_UDP, V4_TCP, V6_UDP, V6_TCP]
+    for i in range(n):
+        kind = kinds[rng.integers(0, 4)]
+        vlan = int(rng.integers(0, 3))
+        need = 14 + 4 * vlan + (20 if kind[0] == 4 else 40) + (8 if kind[1] == UDP else 20)
+        L = int(rng.integers(need, max(need + 1, max_len)))
+        if rng.random() < 0.5:
+            L = int(rng.integers(need, need + 64))
+        fr = build_frames(rng, 1, kind, L, vlan)[0]
+        r = rng.random()
+        if r < 0.15:  # truncate anywhere, including to 0 (BadOffset / OutOfBuffer)
+            fr = fr[: int(rng.integers(0, len(fr) + 1))]
+        elif r < 0.22:  # wrong ether_type
+            et_at = 12 + 4 * vlan
+            fr[et_at : et_at + 2] = rng.integers(0, 256, 2, dtype=np.uint8)
+        elif r < 0.30:  # wrong L4 protocol
+            p_at = 14 + 4 * vlan + (9 if kind[0] == 4 else 6)
+            fr[p_at] = rng.choice([0, 1, 6, 17, 58, 132, 255])
+        elif r < 0.36:  # corrupt a byte (checksum mismatch)
+            j = int(rng.integers(0, len(fr)))
+            fr[j] ^= np.uint8(1 + rng.integers(0, 255))
+        elif r < 0.40:  # all-zero payload region (checksum 0 / 0xFFFF cases)
+            fr[need:] = 0
+        frames.append(bytes(fr))
+    # unaligned placement with random gaps
+    gaps = rng.integers(0, 8, n)
+    off = np.zeros(n, np.uint64)
+    pos = int(rng.integers(0, 4))
+    for i, fr in enumerate(frames):
+        off[i] = pos
+        pos += len(fr) + int(gaps[i])
+    arena = rng.integers(0, 256, size=pos + 16, dtype=np.uint8)  # junk between packets
+    for i, fr in enumerate(frames):
+        arena[int(off[i]) : int(off[i]) + len(fr)] = np.frombuffer(fr, np.uint8)
+    lens = np.array([len(f) for f in frames], np.uint16)
+    return arena, off.astype(np.uint32), lens

@@ -1,0 +1,224 @@
+/*
+ * capsule_gpu.h — C ABI of the MI355X-native packet hot path.
+ *
+ * This header is the drop-in boundary: it is a sibling of Capsule's DPDK
+ * binding header (reference ffi/src/bindings.h:42-89, shim.c:19-64) and is
+ * meant to be bound the same way (bindgen with an allow-list `cgpu_.*`, see
+ * INTEGRATION.md).  Every entry point takes plain pointers and sizes; no HIP
+ * or torch type appears in a signature (streams are passed as `void*`, i.e.
+ * a hipStream_t, NULL = the legacy default stream).
+ *
+ * Error convention (mirrors reference core/src/ffi.rs:86-141 `ToResult` and
+ * core/src/dpdk/mod.rs:62-70): functions return 0 on success and a negative
+ * errno-style code on failure; the same code is kept in a thread-local that
+ * `cgpu_last_error()` returns (the `_rte_errno()` analogue, ffi/src/shim.c:24).
+ * Per-packet failures are never a call failure: they are reported in the
+ * per-packet status byte (CGPU_PKT_*), which mirrors the reference's
+ * `BufferError::{BadOffset,OutOfBuffer}` (core/src/dpdk/mbuf.rs:85-98) and the
+ * "not an IPv4/IPv6/UDP/TCP packet." errors (ip/v4.rs:430, ip/v6/mod.rs:277,
+ * udp.rs:290, tcp.rs:561).
+ *
+ * Ownership (reference core/src/dpdk/mbuf.rs:467-479, 420-424): the library
+ * only BORROWS packet bytes for the duration of a call and never frees or
+ * retains caller memory.
+ */
+#ifndef CAPSULE_GPU_H
+#define CAPSULE_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CGPU_ABI_VERSION 1
+
+/* ---- call-level return codes (negative errno style) -------------------- */
+#define CGPU_OK 0
+#define CGPU_EINVAL (-22)  /* bad argument (null pointer, size overflow) */
+#define CGPU_ENOMEM (-12)  /* device or pinned host allocation failed      */
+#define CGPU_ENODEV (-19)  /* no such HIP device                           */
+#define CGPU_EIO (-5)      /* a HIP runtime call failed                    */
+#define CGPU_ENOSPC (-28)  /* nat64 port table is full                     */
+
+/* ---- per-packet parse status (low byte of `meta`) -----------------------
+ * The first layer of the reference chain Ethernet -> Ipv4|Ipv6 -> Udp|Tcp
+ * that fails decides the code; OK means all three layers parsed.          */
+enum cgpu_pkt_status {
+  CGPU_PKT_OK = 0,
+  /* Ethernet::try_parse (ethernet.rs:279-300) */
+  CGPU_PKT_ETH_BAD_OFFSET = 1,   /* read_data(0): BadOffset(0, data_len)     */
+  CGPU_PKT_ETH_OUT_OF_BUFFER = 2, /* OutOfBuffer(14 or header_len, data_len) */
+  /* Ipv4/Ipv6::try_parse (ip/v4.rs:427-442, ip/v6/mod.rs:274-289) */
+  CGPU_PKT_NOT_IPV4 = 3,         /* "not an IPv4 packet."                    */
+  CGPU_PKT_NOT_IPV6 = 4,         /* "not an IPv6 packet."                    */
+  CGPU_PKT_NOT_IP = 5,           /* neither, when both were accepted        */
+  CGPU_PKT_L3_BAD_OFFSET = 6,
+  CGPU_PKT_L3_OUT_OF_BUFFER = 7,
+  /* Udp/Tcp::try_parse (udp.rs:287-302, tcp.rs:558-573) */
+  CGPU_PKT_NOT_UDP = 8,          /* "not a UDP packet."                      */
+  CGPU_PKT_NOT_TCP = 9,          /* "not a TCP packet."                      */
+  CGPU_PKT_NOT_L4 = 10,          /* neither, when both were accepted        */
+  CGPU_PKT_L4_BAD_OFFSET = 11,
+  CGPU_PKT_L4_OUT_OF_BUFFER = 12,
+  /* nat64 only */
+  CGPU_PKT_NOT_RESIZED = 13,     /* Mbuf::extend NotResized (mbuf.rs:225-233) */
+  CGPU_PKT_TABLE_FULL = 14,      /* port table capacity exhausted            */
+  CGPU_PKT_STATUS_COUNT = 15
+};
+
+/* ---- `meta` word layout (one u32 per packet) ---------------------------- */
+#define CGPU_META_STATUS(m) ((m) & 0xffu)        /* enum cgpu_pkt_status     */
+#define CGPU_META_ETH_LEN(m) (((m) >> 8) & 0xffu) /* 14 / 18 / 22, 0 if none  */
+#define CGPU_META_L3(m) (((m) >> 16) & 0x3u)      /* 0 none, 1 IPv4, 2 IPv6   */
+#define CGPU_META_L4(m) (((m) >> 18) & 0x3u)      /* 0 none, 1 UDP, 2 TCP     */
+#define CGPU_META_IP_CSUM_OK (1u << 20)           /* stored == computed       */
+#define CGPU_META_L4_CSUM_OK (1u << 21)           /* stored == computed       */
+#define CGPU_META_DOT1Q (1u << 22)                /* Ethernet::is_dot1q       */
+#define CGPU_META_QINQ (1u << 23)                 /* Ethernet::is_qinq        */
+#define CGPU_L3_NONE 0u
+#define CGPU_L3_IPV4 1u
+#define CGPU_L3_IPV6 2u
+#define CGPU_L4_NONE 0u
+#define CGPU_L4_UDP 1u
+#define CGPU_L4_TCP 2u
+
+/* ---- parse flags --------------------------------------------------------
+ * ACCEPT_* select which typed parses the caller would have written
+ * (`parse::<Ipv4>()`, `parse::<Udp4>()` ...).  With both L3 (or both L4)
+ * types accepted the kernel dispatches on ether_type / protocol the way a
+ * `group_by` over them would (batch/group_by.rs:143-172).                 */
+#define CGPU_F_ACCEPT_V4 (1u << 0)
+#define CGPU_F_ACCEPT_V6 (1u << 1)
+#define CGPU_F_ACCEPT_UDP (1u << 2)
+#define CGPU_F_ACCEPT_TCP (1u << 3)
+#define CGPU_F_ACCEPT_ALL 0xfu
+#define CGPU_F_CSUM_IP (1u << 4)   /* Ipv4::compute_checksum (v4.rs:322-333) */
+#define CGPU_F_CSUM_L4 (1u << 5)   /* Udp/Tcp::compute_checksum              */
+#define CGPU_F_FLOW_HASH (1u << 6) /* SipHash-1-3(0,0) of `Flow` */
+
+/* ---- batch descriptor ---------------------------------------------------
+ * A batch is an arena of packet bytes plus one (offset, data_len) pair per
+ * packet: the device image of a burst of single-segment mbufs
+ * (buf_addr + data_off, data_len; mbuf.rs:196-205).  All pointers are
+ * device pointers for the *_batch entry points.  arena_len must be < 2^32.  */
+typedef struct cgpu_batch {
+  const uint8_t *arena;
+  uint64_t arena_len;
+  const uint32_t *off; /* [n] byte offset of packet i in the arena */
+  const uint16_t *len; /* [n] data_len of packet i                 */
+  uint32_t n;
+} cgpu_batch;
+
+/* Parsed header fields of one packet, host byte order.  Filled only when
+ * requested; fields of layers that did not parse are zero.  96 bytes.     */
+typedef struct cgpu_hdr_record {
+  uint8_t dst_mac[6];          /*  0 Ethernet::dst                         */
+  uint8_t src_mac[6];          /*  6 Ethernet::src                         */
+  uint16_t ether_type;         /* 12 Ethernet::ether_type (VLAN aware)     */
+  uint8_t eth_len;             /* 14 Ethernet::header_len                  */
+  uint8_t vlan;                /* 15 0 none, 1 802.1Q, 2 802.1ad           */
+  uint8_t version;             /* 16 Ipv4/Ipv6::version                    */
+  uint8_t ihl;                 /* 17 Ipv4::ihl                             */
+  uint8_t dscp;                /* 18                                       */
+  uint8_t ecn;                 /* 19                                       */
+  uint16_t ip_length;          /* 20 Ipv4::total_length / Ipv6::payload_length */
+  uint16_t identification;     /* 22 Ipv4::identification                  */
+  uint8_t ip_flags;            /* 24 bit0 dont_fragment, bit1 more_fragments */
+  uint8_t ttl;                 /* 25 Ipv4::ttl / Ipv6::hop_limit           */
+  uint16_t fragment_offset;    /* 26 Ipv4::fragment_offset                 */
+  uint8_t protocol;            /* 28 Ipv4::protocol / Ipv6::next_header    */
+  uint8_t pad0;                /* 29                                       */
+  uint16_t ip_checksum;        /* 30 Ipv4::checksum (stored)               */
+  uint32_t flow_label;         /* 32 Ipv6::flow_label                      */
+  uint32_t pad1;               /* 36                                       */
+  uint8_t src_ip[16];          /* 40 v4 uses the first 4 bytes             */
+  uint8_t dst_ip[16];          /* 56                                       */
+  uint16_t src_port;           /* 72                                       */
+  uint16_t dst_port;           /* 74                                       */
+  uint16_t udp_length_or_window; /* 76 Udp::length / Tcp::window           */
+  uint16_t l4_checksum;        /* 78 Udp::checksum / Tcp::checksum (stored) */
+  uint32_t seq_no;             /* 80 Tcp::seq_no                           */
+  uint32_t ack_no;             /* 84 Tcp::ack_no                           */
+  uint8_t data_offset;         /* 88 Tcp::data_offset                      */
+  uint8_t tcp_flags;           /* 89 CWR..FIN = 0x80..0x01                 */
+  uint8_t ns;                  /* 90 Tcp::ns                               */
+  uint8_t pad2;                /* 91                                       */
+  uint16_t urgent_pointer;     /* 92                                       */
+  uint16_t pad3;               /* 94                                       */
+} cgpu_hdr_record;
+
+/* Outputs of cgpu_parse_batch, all device pointers with n entries.       */
+typedef struct cgpu_parse_out {
+  uint32_t *meta;       /* required                                          */
+  uint32_t *csum;       /* ip_calc | l4_calc << 16; required with CSUM flags  */
+  uint64_t *flow_hash;  /* required with CGPU_F_FLOW_HASH                     */
+  cgpu_hdr_record *fields; /* optional (NULL = skip field extraction)        */
+} cgpu_parse_out;
+
+typedef struct cgpu_ctx cgpu_ctx;
+
+/* ---- context ------------------------------------------------------------
+ * One context per core thread / RX queue (reference runtime/core_map.rs:
+ * 236-293: shared-nothing).  Contexts are independent; the library keeps
+ * no global locks on the launch path.                                     */
+int cgpu_ctx_create(int hip_device, cgpu_ctx **out);
+void cgpu_ctx_destroy(cgpu_ctx *ctx);
+
+/* Batched Ethernet -> IPv4/IPv6 -> UDP/TCP parse + checksum + flow hash.
+ * Replaces the per-packet chain Mbuf::parse::<Ethernet>() (ethernet.rs:279)
+ * -> parse::<Ipv4|Ipv6>() (v4.rs:427 / v6/mod.rs:274) -> parse::<Udp|Tcp>()
+ * (udp.rs:287 / tcp.rs:558), plus Ipv4::compute_checksum (v4.rs:322),
+ * Udp/Tcp::compute_checksum (udp.rs:204 / tcp.rs:462) evaluated on the bytes
+ * as they are, and the hash of Udp/Tcp::flow() (udp.rs:151, tcp.rs:409).
+ * Asynchronous on `stream`.                                               */
+int cgpu_parse_batch(cgpu_ctx *ctx, const cgpu_batch *batch, uint32_t flags,
+                     const cgpu_parse_out *out, void *stream);
+
+/* Host-memory variant for the DPDK seam: gathers `n` host packets (e.g.
+ * rte_mbuf data addresses, mbuf.rs:202-205) into pinned staging, copies to
+ * the device, parses, and copies the outputs back into HOST arrays (any of
+ * csum / flow_hash / fields may be NULL).  Synchronous.                    */
+int cgpu_parse_host(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *len,
+                    uint32_t n, uint32_t flags, uint32_t *meta, uint32_t *csum,
+                    uint64_t *flow_hash, cgpu_hdr_record *fields);
+
+/* ---- examples/nat64 6to4 -------------------------------------------------
+ * Stateful IPv6 -> IPv4 rewrite of examples/nat64/main.rs:121-150, with the
+ * port map of :37-53 held on the device.  NEXT_PORT starts at `first_port`
+ * (1025 in the reference) and wraps modulo 2^16 like AtomicU16::fetch_add. */
+typedef struct cgpu_portmap cgpu_portmap;
+
+/* capacity_log2: table slots = 2^capacity_log2 (keep load < 0.5).         */
+int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_port,
+                        cgpu_portmap **out);
+void cgpu_portmap_destroy(cgpu_portmap *pm);
+/* Synchronous reads of the map state (test/debug helpers).               */
+int cgpu_portmap_next_port(cgpu_portmap *pm, uint16_t *next_port);
+int cgpu_portmap_size(cgpu_portmap *pm, uint32_t *entries);
+
+/* Disposition per packet (reference batch/mod.rs:54-107, filter_map.rs:73):
+ * ACT = Either::Keep (emitted), DROP = Either::Drop, ABORT = Err.          */
+enum cgpu_disposition { CGPU_ACT = 0, CGPU_DROP = 1, CGPU_ABORT = 2 };
+
+/* in:  device batch of frames.  out_arena/out_off: where frame i is written
+ * (out_off[i] must leave room for len[i] bytes; out_arena must not overlap
+ * the input arena).  out_len[i] = new data_len for ACT packets.
+ * disposition[i] = enum cgpu_disposition; status[i] = enum cgpu_pkt_status
+ * explaining an ABORT.  All device pointers; asynchronous on `stream`.     */
+int cgpu_nat64_6to4(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in,
+                    uint8_t *out_arena, uint64_t out_arena_len, const uint32_t *out_off,
+                    uint16_t *out_len, uint8_t *disposition, uint8_t *status, void *stream);
+
+/* ---- errors -------------------------------------------------------------- */
+int cgpu_last_error(void);
+const char *cgpu_strerror(int code);
+const char *cgpu_pkt_status_str(int status);
+int cgpu_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CAPSULE_GPU_H */

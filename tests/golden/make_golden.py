@@ -1,0 +1,137 @@
+"""Regenerate the committed golden fixtures from the reference's own test data.
+
+Run in the build container only (it reads /root/reference, which does not
+exist on the GPU box):
+
+    python tests/golden/make_golden.py
+
+Outputs (all data, no reference source):
+  reference_packets.json  byte arrays of core/src/testils/byte_arrays.rs and
+                          the packets inside examples/pktdump/tcp{4,6}.pcap and
+                          examples/ping4d/echo.pcap, as hex
+  reference_kats.json     the values the reference's unit tests assert on
+                          those packets, each with the file:line of the assert
+
+The reference is Rust + DPDK and cannot be built or run here,
+so these fixtures are the oracle's pin.  The Rust source is only read as text
+to lift the byte arrays out; the asserted values below are transcribed from
+the cited test functions.
+"""
+import json
+import pathlib
+import re
+import struct
+
+REF = pathlib.Path("/root/reference")
+OUT = pathlib.Path(__file__).resolve().parent
+
+ARRAYS = REF / "core/src/testils/byte_arrays.rs"
+PCAPS = {
+    "pktdump_tcp4": "examples/pktdump/tcp4.pcap",
+    "pktdump_tcp6": "examples/pktdump/tcp6.pcap",
+    "ping4d_echo": "examples/ping4d/echo.pcap",
+}
+
+
+def lift_arrays():
+    text = ARRAYS.read_text()
+    out = {}
+    pat = re.compile(r"pub const (\w+): \[u8; (\d+)\] = \[(.*?)\];", re.S)
+    for m in pat.finditer(text):
+        name, n, body = m.group(1), int(m.group(2)), m.group(3)
+        body = re.sub(r"//[^\n]*", "", body)
+        vals = [int(t, 16) for t in re.findall(r"0x[0-9a-fA-F]{2}", body)]
+        assert len(vals) == n, (name, len(vals), n)
+        line = text[: m.start()].count("\n") + 1
+        out[name] = {
+            "hex": bytes(vals).hex(),
+            "len": n,
+            "source": f"core/src/testils/byte_arrays.rs:{line}",
+        }
+    return out
+
+
+def lift_pcap(rel):
+    data = (REF / rel).read_bytes()
+    magic = struct.unpack("<I", data[:4])[0]
+    endian = "<" if magic in (0xA1B2C3D4, 0xA1B23C4D) else ">"
+    pos, pkts = 24, []
+    while pos + 16 <= len(data):
+        _, _, incl, _ = struct.unpack(endian + "IIII", data[pos : pos + 16])
+        pos += 16
+        pkts.append(data[pos : pos + incl].hex())
+        pos += incl
+    return {"packets": pkts, "source": rel}
+
+
+# Values asserted by the reference's tests, keyed by fixture.  "ip_csum" /
+# "l4_csum" are the values compute_checksum()/reconcile() must reproduce.
+KATS = [
+    {"packet": "IPV4_UDP_PACKET", "src": "core/src/packets/ethernet.rs:497-506",
+     "expect": {"dst_mac": "000000000001", "src_mac": "000000000002", "ether_type": 0x0800,
+                "eth_len": 14}},
+    {"packet": "VLAN_DOT1Q_PACKET", "src": "core/src/packets/ethernet.rs:507-516",
+     "expect": {"dst_mac": "000000000001", "src_mac": "000000000002", "vlan": 1,
+                "ether_type": 0x0806, "eth_len": 18}},
+    {"packet": "VLAN_QINQ_PACKET", "src": "core/src/packets/ethernet.rs:519-528",
+     "expect": {"dst_mac": "000000000001", "src_mac": "000000000002", "vlan": 2,
+                "ether_type": 0x0806, "eth_len": 22}},
+    {"packet": "IPV4_UDP_PACKET", "src": "core/src/packets/ip/v4.rs:624-643",
+     "expect": {"version": 4, "ihl": 5, "ip_length": 38, "identification": 43849,
+                "dont_fragment": 1, "more_fragments": 0, "fragment_offset": 0, "dscp": 0,
+                "ecn": 0, "ttl": 255, "protocol": 17, "ip_checksum": 0xF700,
+                "src_ip": "8b85d96e", "dst_ip": "8b85e902"}},
+    {"packet": "IPV4_UDP_PACKET", "src": "core/src/packets/ip/v4.rs:718-728",
+     "expect": {"ip_csum": 0xF700}},
+    {"packet": "IPV6_TCP_PACKET", "src": "core/src/packets/ip/v4.rs:646-651",
+     "parse": "v4", "status": "NOT_IPV4"},
+    {"packet": "IPV6_TCP_PACKET", "src": "core/src/packets/ip/v6/mod.rs:479-493",
+     "expect": {"version": 6, "dscp": 0, "ecn": 0, "flow_label": 0, "ip_length": 24,
+                "protocol": 6, "ttl": 2,
+                "src_ip": "20010db885a300000000000000000001",
+                "dst_ip": "20010db885a3000000008a2e03707334"}},
+    {"packet": "IPV4_UDP_PACKET", "src": "core/src/packets/ip/v6/mod.rs:495-500",
+     "parse": "v6", "status": "NOT_IPV6"},
+    {"packet": "IPV4_UDP_PACKET", "src": "core/src/packets/udp.rs:386-397",
+     "expect": {"src_port": 39376, "dst_port": 1087, "udp_length": 18, "l4_checksum": 0x7228}},
+    {"packet": "IPV4_TCP_PACKET", "src": "core/src/packets/udp.rs:400-406",
+     "parse": "udp", "status": "NOT_UDP"},
+    {"packet": "IPV4_UDP_PACKET", "src": "core/src/packets/udp.rs:409-421",
+     "expect": {"flow": ["8b85d96e", "8b85e902", 39376, 1087, 17]}},
+    {"packet": "IPV4_UDP_PACKET", "src": "core/src/packets/udp.rs:447-457",
+     "expect": {"l4_csum": 0x7228}},
+    {"packet": "IPV4_TCP_PACKET", "src": "core/src/packets/tcp.rs:679-702",
+     "expect": {"src_port": 36869, "dst_port": 23, "seq_no": 1913975060, "ack_no": 0,
+                "data_offset": 6, "window": 8760, "l4_checksum": 0xA92C, "urgent_pointer": 0,
+                "ns": 0, "tcp_flags": 0x02}},
+    {"packet": "IPV4_UDP_PACKET", "src": "core/src/packets/tcp.rs:705-711",
+     "parse": "tcp", "status": "NOT_TCP"},
+    {"packet": "IPV4_TCP_PACKET", "src": "core/src/packets/tcp.rs:714-726",
+     "expect": {"flow": ["8b85d96e", "8b85e902", 36869, 23, 6]}},
+    {"packet": "IPV4_TCP_PACKET", "src": "core/src/packets/tcp.rs:768-778",
+     "expect": {"l4_csum": 0xA92C}},
+    # Not asserted by the reference, re-derived in SURVEY.md Appendix B with an
+    # independent Python restatement; kept as regression values.
+    {"packet": "IPV4_TCP_PACKET", "src": "byte_arrays.rs:104 comment; SURVEY.md App. B",
+     "expect": {"ip_csum": 0x9997}},
+    {"packet": "ICMPV4_PACKET", "src": "SURVEY.md Appendix B (icmp/v4/mod.rs:469 fixture)",
+     "parse": "v4", "expect": {"ip_csum": 0x2B73}},
+]
+
+# checksum.rs:226-229
+INC_KATS = [{"old": 0xDD2F, "old_value": [0x5555], "new_value": [0x3285], "expect": 0x0000,
+             "src": "core/src/packets/checksum.rs:226-229"}]
+
+
+def main():
+    pk = lift_arrays()
+    for key, rel in PCAPS.items():
+        pk[key] = lift_pcap(rel)
+    (OUT / "reference_packets.json").write_text(json.dumps(pk, indent=1, sort_keys=True) + "\n")
+    (OUT / "reference_kats.json").write_text(
+        json.dumps({"kats": KATS, "compute_inc": INC_KATS}, indent=1) + "\n")
+    print("wrote", len(pk), "packet fixtures,", len(KATS), "KATs")
+
+
+if __name__ == "__main__":
+    main()

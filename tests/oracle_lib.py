@@ -1,0 +1,113 @@
+"""ctypes handle on the CPU oracle (oracle/liboracle.so) — test-side only.
+
+The oracle is the parity checker: tests, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg are the only users (oracle/oracle.h).
+"""
+import ctypes
+import pathlib
+import subprocess
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+ORACLE_DIR = ROOT / "oracle"
+
+
+def load(name="liboracle.so"):
+    path = ORACLE_DIR / name
+    if not path.exists():
+        subprocess.run(["make", "-C", str(ORACLE_DIR), name], check=True,
+                       stdout=subprocess.DEVNULL)
+    L = ctypes.CDLL(str(path))
+    vp, u8, u16, u32, u64, sz, i32 = (ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint16,
+                                      ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t,
+                                      ctypes.c_int)
+    L.or_compute.restype = u16
+    L.or_compute.argtypes = [u16, vp, sz]
+    L.or_compute_inc.restype = u16
+    L.or_compute_inc.argtypes = [u16, vp, vp, sz]
+    L.or_pseudo_v4.restype = u16
+    L.or_pseudo_v4.argtypes = [u32, u32, u16, u8]
+    L.or_pseudo_v6.restype = u16
+    L.or_pseudo_v6.argtypes = [vp, vp, u16, u8]
+    L.or_siphash.restype = u64
+    L.or_siphash.argtypes = [i32, i32, u64, u64, vp, sz]
+    L.or_flow_bytes.restype = sz
+    L.or_flow_bytes.argtypes = [i32, vp, vp, u16, u16, u8, vp]
+    L.or_flow_hash.restype = u64
+    L.or_flow_hash.argtypes = [i32, vp, vp, u16, u16, u8]
+    L.or_parse_batch.restype = None
+    L.or_parse_batch.argtypes = [vp, vp, vp, u32, u32, vp, vp, vp, vp]
+    L.or_multi_parse_udp.restype = u32
+    L.or_multi_parse_udp.argtypes = [vp, vp, vp, u32]
+    L.or_portmap_new.restype = vp
+    L.or_portmap_new.argtypes = [u16]
+    L.or_portmap_free.restype = None
+    L.or_portmap_free.argtypes = [vp]
+    L.or_portmap_next_port.restype = u16
+    L.or_portmap_next_port.argtypes = [vp]
+    L.or_portmap_size.restype = u32
+    L.or_portmap_size.argtypes = [vp]
+    L.or_nat64_6to4.restype = None
+    L.or_nat64_6to4.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
+    return L
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = load()
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data if a is not None else None
+
+
+def parse_batch(arena, off, length, flags, fields=True):
+    """Oracle parse -> (meta u32, csum u32, hash u64, fields bytes [n,96])."""
+    n = len(off)
+    arena = np.ascontiguousarray(arena, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    length = np.ascontiguousarray(length, np.uint16)
+    meta = np.zeros(n, np.uint32)
+    csum = np.zeros(n, np.uint32)
+    h = np.zeros(n, np.uint64)
+    fl = np.zeros((n, 96), np.uint8) if fields else None
+    lib().or_parse_batch(_p(arena), _p(off), _p(length), n, flags, _p(meta), _p(csum), _p(h),
+                         _p(fl))
+    return meta, csum, h, fl
+
+
+class PortMap:
+    def __init__(self, first_port=1025):
+        self.h = lib().or_portmap_new(first_port)
+
+    def next_port(self):
+        return lib().or_portmap_next_port(self.h)
+
+    def size(self):
+        return lib().or_portmap_size(self.h)
+
+    def nat_6to4(self, arena, off, length, out_off=None, out_size=None):
+        n = len(off)
+        arena = np.ascontiguousarray(arena, np.uint8)
+        off = np.ascontiguousarray(off, np.uint32)
+        length = np.ascontiguousarray(length, np.uint16)
+        out_off = off if out_off is None else np.ascontiguousarray(out_off, np.uint32)
+        out = np.zeros(out_size or len(arena), np.uint8)
+        out_len = np.zeros(n, np.uint16)
+        disp = np.zeros(n, np.uint8)
+        st = np.zeros(n, np.uint8)
+        lib().or_nat64_6to4(self.h, _p(arena), _p(off), _p(length), n, _p(out), _p(out_off),
+                            _p(out_len), _p(disp), _p(st))
+        return out, out_len, disp, st
+
+    def __del__(self):
+        try:
+            lib().or_portmap_free(self.h)
+        except Exception:
+            pass

@@ -1,0 +1,75 @@
+"""The C-ABI library loads and exports every symbol include/capsule_gpu.h
+declares (no GPU work: only the pure-host entry points are called)."""
+import ctypes
+import pathlib
+import re
+import subprocess
+
+from capsule_amd import _native as N
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+def declared_functions():
+    names = set()
+    for h in (ROOT / "include").glob("*.h"):
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        names |= set(re.findall(r"\b(cgpu_\w+)\s*\(", text))
+    return names
+
+
+def test_header_declares_what_binding_binds():
+    assert declared_functions() == set(N.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = N.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", str(N.LIB_PATH)], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\b(cgpu_\w+)\b", out))
+    assert declared_functions() <= exported
+
+
+def test_library_is_gfx950_hip_code():
+    """The shared object carries a gfx950 HIP fat binary (no other target)."""
+    data = N.LIB_PATH.read_bytes()
+    assert b".hip_fatbin" in data
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in data
+    assert b"--gfx942" not in data and b"--gfx90a" not in data
+
+
+def test_host_only_entry_points():
+    L = N.lib()
+    assert L.cgpu_abi_version() == N.ABI_VERSION
+    assert L.cgpu_strerror(N.EINVAL) == b"invalid argument"
+    assert L.cgpu_strerror(N.OK) == b"success"
+    # the reference's own error strings (ip/v4.rs:430, v6/mod.rs:277, udp.rs:290, tcp.rs:561)
+    assert L.cgpu_pkt_status_str(N.PKT["NOT_IPV4"]) == b"not an IPv4 packet."
+    assert L.cgpu_pkt_status_str(N.PKT["NOT_IPV6"]) == b"not an IPv6 packet."
+    assert L.cgpu_pkt_status_str(N.PKT["NOT_UDP"]) == b"not a UDP packet."
+    assert L.cgpu_pkt_status_str(N.PKT["NOT_TCP"]) == b"not a TCP packet."
+    for s, name in enumerate(N.PKT_STATUS):
+        assert L.cgpu_pkt_status_str(s) != b"unknown status", name
+
+
+def test_null_arguments_fail_with_einval_and_set_last_error():
+    L = N.lib()
+    assert L.cgpu_parse_batch(None, None, 0, None, None) == N.EINVAL
+    assert L.cgpu_last_error() == N.EINVAL
+    out = ctypes.c_void_p()
+    assert L.cgpu_portmap_create(None, 20, 1025, ctypes.byref(out)) == N.EINVAL
+    assert L.cgpu_nat64_6to4(None, None, None, None, 0, None, None, None, None, None) == N.EINVAL
+
+
+def test_record_layout_matches_header():
+    import numpy as np
+
+    dt = np.dtype(N.HDR_RECORD_FIELDS)
+    assert dt.itemsize == N.HDR_RECORD_SIZE == 96
+    for field, off in (("ether_type", 12), ("ip_length", 20), ("protocol", 28),
+                       ("ip_checksum", 30), ("flow_label", 32), ("src_ip", 40), ("dst_ip", 56),
+                       ("src_port", 72), ("l4_checksum", 78), ("seq_no", 80), ("data_offset", 88),
+                       ("urgent_pointer", 92)):
+        assert dt.fields[field][1] == off, field

@@ -1,0 +1,138 @@
+"""Parity of the HIP nat64 6to4 rewrite with the oracle's restatement of
+examples/nat64/main.rs:121-150 (port map :37-53), including port-map state
+carried across consecutive batches, drops, aborts, VLAN frames, unaligned
+output slots and NEXT_PORT wrap-around."""
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib
+from capsule_amd import _native as N
+from capsule_amd import synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def run_pair(ctx, batches, first_port=1025, cap_log2=16, out_shift=0):
+    """Feed the same batches to the GPU gateway and the oracle; compare all."""
+    from capsule_amd import packets
+
+    gw = packets.Nat64Gateway(ctx, capacity_log2=cap_log2, first_port=first_port)
+    pm = oracle_lib.PortMap(first_port)
+    for arena, off, ln in batches:
+        out_off = off.astype(np.uint32) + np.uint32(out_shift)
+        size = len(arena) + out_shift + 64
+        b = packets.PacketBatch.from_numpy(arena, off, ln, DEV)
+        out_arena = torch.zeros(size, dtype=torch.uint8, device=DEV)
+        oo = torch.from_numpy(out_off.view(np.int32)).to(DEV)
+        ob, disp, st = gw.nat_6to4(b, out_arena=out_arena, out_off=oo)
+        torch.cuda.synchronize()
+        g_out = out_arena.cpu().numpy()
+        g_len = ob.len.cpu().numpy().view(np.uint16)
+        g_disp = disp.cpu().numpy()
+        g_st = st.cpu().numpy()
+        o_out, o_len, o_disp, o_st = pm.nat_6to4(arena, off, ln, out_off, size)
+        bad = np.nonzero(g_disp != o_disp)[0]
+        assert not len(bad), f"disposition differs at {bad[:8]}: {g_disp[bad[:4]]} vs {o_disp[bad[:4]]}"
+        bad = np.nonzero(g_st != o_st)[0]
+        assert not len(bad), f"status differs at {bad[:8]}: {g_st[bad[:4]]} vs {o_st[bad[:4]]}"
+        assert (g_len == o_len).all()
+        for i in np.nonzero(o_disp == N.ACT)[0]:
+            a, L = int(out_off[i]), int(o_len[i])
+            if not (g_out[a : a + L] == o_out[a : a + L]).all():
+                j = np.nonzero(g_out[a : a + L] != o_out[a : a + L])[0]
+                raise AssertionError(f"frame {i} differs at bytes {j[:8]}")
+        assert gw.next_port() == pm.next_port()
+        assert gw.size() == pm.size()
+    return gw, pm
+
+
+def test_single_batch_parity(ctx):
+    run_pair(ctx, [synth.nat64_stream(20000, n_keys=3000)])
+
+
+def test_port_map_persists_across_batches(ctx):
+    """A stream cut into consecutive batches gets the ports the reference's
+    single-core pipeline would assign (first-seen order over the stream)."""
+    a, o, l = synth.nat64_stream(40000, n_keys=5000, seed=3)
+    cuts = [0, 1, 100, 7000, 25000, 40000]
+    batches = []
+    for s, e in zip(cuts[:-1], cuts[1:]):
+        base = int(o[s])
+        end = int(o[e - 1]) + int(l[e - 1])
+        batches.append((a[base:end], o[s:e] - np.uint32(base), l[s:e]))
+    run_pair(ctx, batches)
+
+
+def test_drops_aborts_vlan_and_odd_lengths(ctx):
+    rng = np.random.default_rng(8)
+    frames = []
+    keys = rng.integers(0, 256, size=(50, 16), dtype=np.uint8)
+    for i in range(3000):
+        vlan = int(rng.integers(0, 3))
+        L = int(rng.integers(14 + 4 * vlan + 60, 400))
+        kind = synth.V6_TCP if rng.random() < 0.8 else [synth.V6_UDP, synth.V4_TCP][i % 2]
+        fr = synth.build_frames(rng, 1, kind, L, vlan, hop_limit_min=1)[0]
+        if kind == synth.V6_TCP:
+            o6 = 14 + 4 * vlan
+            fr[o6 + 8 : o6 + 24] = keys[rng.integers(0, 50)]
+            fr[o6 + 40 : o6 + 42] = rng.integers(0, 4, 2, dtype=np.uint8)
+        r = rng.random()
+        if r < 0.05:
+            fr = fr[: int(rng.integers(0, len(fr)))]  # truncated: Abort at some layer
+        elif r < 0.08:
+            fr[14 + 4 * vlan + 7] = 0  # hop_limit 0: wraps to ttl 255 (release build)
+        frames.append(bytes(fr))
+    # the largest frame an mbuf holds (2048-B data room): remove 40 + push 20
+    # always fits, so Mbuf::extend's NotResized is unreachable here
+    frames.append(bytes(synth.build_frames(rng, 1, synth.V6_TCP, 2048, 0, 1)[0]))
+    arena, off, ln = synth.pack_frames(frames, slot=64)
+    run_pair(ctx, [(arena, off, ln)])
+    _, _, disp, st = oracle_lib.PortMap().nat_6to4(arena, off, ln)
+    assert {N.ACT, N.DROP, N.ABORT} <= set(disp.tolist())
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_unaligned_output_slots(ctx, shift):
+    run_pair(ctx, [synth.nat64_stream(5000, n_keys=700, seed=11, drop_frac=0.1)],
+             out_shift=shift)
+
+
+def test_next_port_wraps_mod_2_16(ctx):
+    """AtomicU16::fetch_add wraps (examples/nat64/main.rs:42-48)."""
+    gw, pm = run_pair(ctx, [synth.nat64_stream(2000, n_keys=40, seed=12)], first_port=65520)
+    assert gw.next_port() == (65520 + 40) % 65536 == pm.next_port()
+
+
+def test_config4_full_size_properties(ctx):
+    """BASELINE config 4 at 1M x 256 B: every output frame is a reconciled
+    IPv4/TCP packet (GPU parse verifies both checksums), 20 B shorter, payload
+    bytes unchanged, and ports are exactly 1025 + first-seen ordinal."""
+    from capsule_amd import packets
+
+    n, keys = 1 << 20, 50_000
+    a, o, l = synth.nat64_stream(n, n_keys=keys)
+    b = packets.PacketBatch.from_numpy(a, o, l, DEV)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=17)
+    ob, disp, st = gw.nat_6to4(b)
+    r = packets.parse(ctx, ob, flags=N.F_ACCEPT_ALL | N.F_CSUM_IP | N.F_CSUM_L4, fields=True)
+    torch.cuda.synchronize()
+    assert (disp == N.ACT).all() and (st == 0).all()
+    assert (ob.len.cpu().numpy().view(np.uint16) == 236).all()
+    meta = r.meta.cpu().numpy().view(np.uint32)
+    assert (meta & 0xFF == 0).all()
+    assert (meta & N.META_IP_CSUM_OK).all() and (meta & N.META_L4_CSUM_OK).all()
+    out = ob.arena.cpu().numpy().reshape(n, 256)
+    assert (out[:, 54:236] == a.reshape(n, 256)[:, 74:256]).all()
+    # ports: ordinal of first appearance of (src, port) in stream order
+    src = a.reshape(n, 256)[:, 22:38]
+    sport = a.reshape(n, 256)[:, 54:56]
+    key = np.concatenate([src, sport], axis=1).view(np.dtype((np.void, 18))).reshape(-1)
+    _, first, inv = np.unique(key, return_index=True, return_inverse=True)
+    rank = np.empty(len(first), np.int64)
+    rank[np.argsort(first)] = np.arange(len(first))
+    want = (1025 + rank[inv]) & 0xFFFF
+    got = out[:, 34].astype(np.int64) * 256 + out[:, 35]
+    assert (got == want).all()
+    assert gw.size() == len(first) and gw.next_port() == (1025 + len(first)) & 0xFFFF

@@ -1,0 +1,92 @@
+"""Cross-check the C oracle against the independent Python restatement on
+seeded edge-case batches, and the synthetic generators against both."""
+import numpy as np
+import pytest
+
+import oracle_lib
+import pyref
+from capsule_amd import _native as N
+from capsule_amd import synth
+
+ALL = N.F_ACCEPT_ALL | N.F_CSUM_IP | N.F_CSUM_L4 | N.F_FLOW_HASH
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_fuzz_oracle_vs_pyref(seed):
+    arena, off, ln = synth.fuzz(300, seed=seed)
+    for flags in (ALL, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_L4, N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | 0x70):
+        meta, csum, h, _ = oracle_lib.parse_batch(arena, off, ln, flags, fields=False)
+        for i in range(len(off)):
+            fr = bytes(arena[off[i] : off[i] + ln[i]])
+            st, m, ipc, l4c, hh = pyref.parse(fr, flags)
+            assert int(meta[i]) == (m | st), i
+            assert int(csum[i]) == (ipc | l4c << 16), i
+            assert int(h[i]) == hh, i
+
+
+def test_fuzz_covers_every_status():
+    arena, off, ln = synth.fuzz(2000, seed=7)
+    seen = set()
+    for flags in (ALL, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | 0x70, N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | 0x70):
+        meta, _, _, _ = oracle_lib.parse_batch(arena, off, ln, flags, fields=False)
+        seen |= set((meta & 0xFF).tolist())
+    for s in ("OK", "ETH_BAD_OFFSET", "ETH_OUT_OF_BUFFER", "NOT_IPV4", "NOT_IPV6", "NOT_IP",
+              "L3_OUT_OF_BUFFER", "NOT_UDP", "NOT_TCP", "NOT_L4", "L4_OUT_OF_BUFFER"):
+        assert N.PKT[s] in seen, s
+
+
+@pytest.mark.parametrize("gen", ["uniform64", "uniform_vlan", "imix", "nat64"])
+def test_generators_are_reconciled(gen):
+    """Synthetic packets are internally consistent like the proptest strategies
+    (strategy.rs:395-397): every layer parses and every checksum verifies."""
+    if gen == "uniform64":
+        a, o, l = synth.uniform(4096)
+    elif gen == "uniform_vlan":
+        a, o, l = synth.uniform(4096, kind=synth.V6_TCP, frame_len=300, vlan=2, slot=320)
+    elif gen == "imix":
+        a, o, l = synth.imix(8192, vlan_frac=0.2)
+    else:
+        a, o, l = synth.nat64_stream(4096, n_keys=100)
+    meta, csum, h, fl = oracle_lib.parse_batch(a, o, l, ALL, fields=True)
+    assert (meta & 0xFF == 0).all()
+    assert (meta & N.META_L4_CSUM_OK).all()
+    v4 = ((meta >> 16) & 3) == N.L3_IPV4
+    assert (meta[v4] & N.META_IP_CSUM_OK).all()
+    rec = fl.view(np.dtype(N.HDR_RECORD_FIELDS)).reshape(-1)
+    assert (rec["ip_length"][v4] == (l[v4] - rec["eth_len"][v4])).all()
+
+
+def test_multi_parse_udp_counts():
+    a, o, l = synth.uniform(1000)
+    assert oracle_lib.lib().or_multi_parse_udp(a.ctypes.data, o.ctypes.data, l.ctypes.data, 1000) == 1000
+    a, o, l = synth.uniform(1000, kind=synth.V4_TCP, frame_len=64)
+    assert oracle_lib.lib().or_multi_parse_udp(a.ctypes.data, o.ctypes.data, l.ctypes.data, 1000) == 0
+
+
+def test_oracle_under_sanitizers():
+    """Run the oracle's parse and nat64 on edge cases under ASan+UBSan in a
+    subprocess (the sanitizer runtime must be preloaded into a fresh python)."""
+    import os
+    import subprocess
+    import sys
+
+    san = oracle_lib.ORACLE_DIR / "liboracle_san.so"
+    subprocess.run(["make", "-C", str(oracle_lib.ORACLE_DIR), "liboracle_san.so"], check=True,
+                   stdout=subprocess.DEVNULL)
+    asan = subprocess.run(["gcc", "-print-file-name=libasan.so"], capture_output=True,
+                          text=True).stdout.strip()
+    ubsan = subprocess.run(["gcc", "-print-file-name=libubsan.so"], capture_output=True,
+                           text=True).stdout.strip()
+    code = (
+        "import sys; sys.path.insert(0, 'tests'); sys.path.insert(0, '.');"
+        "import oracle_lib as o; o._lib = o.load('liboracle_san.so');"
+        "from capsule_amd import synth;"
+        "a, off, ln = synth.fuzz(400, seed=11); o.parse_batch(a, off, ln, 0x7f);"
+        "a, off, ln = synth.nat64_stream(300, n_keys=50, drop_frac=0.2);"
+        "pm = o.PortMap(); pm.nat_6to4(a, off, ln); print('clean')"
+    )
+    env = dict(os.environ, LD_PRELOAD=f"{asan} {ubsan}", ASAN_OPTIONS="detect_leaks=0",
+               UBSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([sys.executable, "-c", code], cwd=str(oracle_lib.ROOT), env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "clean" in r.stdout, r.stderr[-2000:]

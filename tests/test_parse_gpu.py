@@ -1,0 +1,182 @@
+"""Parity of the HIP parse/checksum/flow-hash kernel with the CPU oracle.
+
+Bit-exact on every output (meta word, both checksums, flow hash, the 96-byte
+header record) for the reference's own fixtures, seeded edge-case batches
+and the BASELINE configurations; full-size runs are checked through
+size-independent properties (every reconciled packet parses and verifies).
+"""
+import json
+import pathlib
+
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib
+from capsule_amd import _native as N
+from capsule_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+GOLD = pathlib.Path(__file__).resolve().parent / "golden"
+ALL = N.F_ACCEPT_ALL | N.F_CSUM_IP | N.F_CSUM_L4 | N.F_FLOW_HASH
+DEV = "cuda:0"
+
+
+def gpu_parse(ctx, arena, off, ln, flags, fields=True):
+    from capsule_amd import packets
+
+    b = packets.PacketBatch.from_numpy(arena, off, ln, DEV)
+    r = packets.parse(ctx, b, flags=flags, fields=fields)
+    torch.cuda.synchronize()
+    meta = r.meta.cpu().numpy().view(np.uint32)
+    csum = r.csum.cpu().numpy().view(np.uint32)
+    h = r.flow_hash.cpu().numpy().view(np.uint64)
+    fl = r.fields.cpu().numpy() if fields else None
+    return meta, csum, h, fl
+
+
+def assert_parity(ctx, arena, off, ln, flags, fields=True):
+    gm, gc, gh, gf = gpu_parse(ctx, arena, off, ln, flags, fields)
+    om, oc, oh, of = oracle_lib.parse_batch(arena, off, ln, flags, fields)
+    bad = np.nonzero(gm != om)[0]
+    assert not len(bad), f"meta differs at {bad[:8]}: gpu {gm[bad[:4]]} oracle {om[bad[:4]]}"
+    if flags & (N.F_CSUM_IP | N.F_CSUM_L4):
+        bad = np.nonzero(gc != oc)[0]
+        assert not len(bad), f"csum differs at {bad[:8]}: gpu {gc[bad[:4]]} oracle {oc[bad[:4]]}"
+    if flags & N.F_FLOW_HASH:
+        bad = np.nonzero(gh != oh)[0]
+        assert not len(bad), f"hash differs at {bad[:8]}"
+    if fields:
+        bad = np.nonzero((gf != of).any(axis=1))[0]
+        assert not len(bad), f"fields differ at {bad[:8]}"
+    return om
+
+
+def test_reference_fixtures_every_flag_combination(ctx):
+    pk = json.loads((GOLD / "reference_packets.json").read_text())
+    frames = [bytes.fromhex(v["hex"]) for v in pk.values() if "hex" in v]
+    for v in pk.values():
+        frames += [bytes.fromhex(h) for h in v.get("packets", [])]
+    arena, off, ln = synth.pack_frames(frames)
+    for acc in range(16):
+        for feat in (0, N.F_CSUM_IP, N.F_CSUM_L4, N.F_FLOW_HASH, 0x70):
+            assert_parity(ctx, arena, off, ln, acc | feat, fields=True)
+    assert_parity(ctx, arena, off, ln, ALL, fields=False)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_fuzz_unaligned_edge_cases(ctx, seed):
+    arena, off, ln = synth.fuzz(3000, seed=seed)
+    for flags in (ALL, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_L4,
+                  N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | N.F_FLOW_HASH, N.F_CSUM_IP | N.F_CSUM_L4):
+        assert_parity(ctx, arena, off, ln, flags, fields=True)
+    assert_parity(ctx, arena, off, ln, ALL, fields=False)
+
+
+def test_every_length_boundary(ctx):
+    """Each kind truncated to every length 0..L, plus jumbo and max-u16 frames,
+    at every arena alignment (BadOffset / OutOfBuffer edges, register-window
+    edge at 96 B, the streamed tail, odd spans)."""
+    rng = np.random.default_rng(9)
+    frames = []
+    for kind in (synth.V4_UDP, synth.V4_TCP, synth.V6_UDP, synth.V6_TCP):
+        for vlan in (0, 1, 2):
+            full = bytes(synth.build_frames(rng, 1, kind, 180, vlan)[0])
+            frames += [full[:L] for L in range(0, 181)]
+    for L in (2047, 2048, 9000, 65535):
+        frames.append(bytes(synth.build_frames(rng, 1, synth.V6_UDP, L, 0)[0]))
+        frames.append(bytes(synth.build_frames(rng, 1, synth.V4_TCP, L, 2)[0]))
+    for shift in range(4):
+        arena, off, ln = synth.pack_frames(frames)
+        arena = np.concatenate([np.zeros(shift, np.uint8), arena])
+        assert_parity(ctx, arena, off + shift, ln, ALL)
+
+
+def test_packet_flush_with_arena_end(ctx):
+    """Packets that end exactly at the end of the arena, at every alignment
+    (the buffer-resource range check must return zeros, not fault)."""
+    rng = np.random.default_rng(10)
+    for L in (42, 60, 64, 97, 150):
+        fr = bytes(synth.build_frames(rng, 1, synth.V4_UDP, L)[0])
+        for shift in range(8):
+            arena = np.concatenate([np.zeros(shift, np.uint8), np.frombuffer(fr, np.uint8)])
+            assert_parity(ctx, arena, np.array([shift], np.uint32), np.array([L], np.uint16), ALL)
+
+
+def test_config2_uniform_64B_1M(ctx):
+    """BASELINE config 2: 1,048,576 x 64-B IPv4/UDP, bit-exact vs the oracle."""
+    arena, off, ln = synth.uniform(1 << 20)
+    om = assert_parity(ctx, arena, off, ln, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP |
+                       N.F_CSUM_L4, fields=False)
+    assert (om & 0xFF == 0).all() and (om & N.META_IP_CSUM_OK).all()
+
+
+def test_config3_imix_parity_and_properties(ctx):
+    """BASELINE config 3: IMIX, bit-exact on 256k packets; the full 1M batch
+    through properties (all parse, all checksums verify, hash never 0)."""
+    arena, off, ln = synth.imix(1 << 18, vlan_frac=0.1)
+    assert_parity(ctx, arena, off, ln, ALL, fields=True)
+    arena, off, ln = synth.imix(1 << 20)
+    gm, gc, gh, _ = gpu_parse(ctx, arena, off, ln, ALL, fields=False)
+    assert (gm & 0xFF == 0).all()
+    assert (gm & N.META_L4_CSUM_OK).all()
+    v4 = ((gm >> 16) & 3) == N.L3_IPV4
+    assert (gm[v4] & N.META_IP_CSUM_OK).all()
+    assert (gh != 0).all()
+    # a sample of 4096 packets spread over the batch, bit-exact
+    idx = np.linspace(0, len(off) - 1, 4096).astype(np.int64)
+    om, oc, oh, _ = oracle_lib.parse_batch(arena, off[idx], ln[idx], ALL, fields=False)
+    assert (gm[idx] == om).all() and (gc[idx] == oc).all() and (gh[idx] == oh).all()
+
+
+def test_parse_is_idempotent_and_stream_ordered(ctx):
+    """Two launches on two streams give identical results (no hidden state)."""
+    from capsule_amd import packets
+
+    arena, off, ln = synth.imix(50000, seed=77)
+    b = packets.PacketBatch.from_numpy(arena, off, ln, DEV)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    r1 = packets.parse(ctx, b, flags=ALL, stream=s1)
+    r2 = packets.parse(ctx, b, flags=ALL, stream=s2)
+    torch.cuda.synchronize()
+    assert torch.equal(r1.meta, r2.meta) and torch.equal(r1.csum, r2.csum)
+    assert torch.equal(r1.flow_hash, r2.flow_hash)
+
+
+def test_host_entry_point_matches_device_entry_point(ctx):
+    from capsule_amd import packets
+
+    arena, off, ln = synth.fuzz(2000, seed=21)
+    frames = [bytes(arena[o : o + l]) for o, l in zip(off, ln)]
+    meta, csum, fh, recs = packets.parse_host(ctx, frames, flags=ALL, fields=True)
+    om, oc, oh, of = oracle_lib.parse_batch(arena, off, ln, ALL, True)
+    assert (meta == om).all() and (csum == oc).all() and (fh == oh).all()
+    assert (recs.view(np.uint8).reshape(-1, 96) == of).all()
+
+
+def test_empty_batch(ctx):
+    from capsule_amd import packets
+
+    b = packets.PacketBatch(torch.zeros(64, dtype=torch.uint8, device=DEV),
+                            torch.zeros(0, dtype=torch.int32, device=DEV),
+                            torch.zeros(0, dtype=torch.int16, device=DEV))
+    r = packets.parse(ctx, b, flags=ALL)
+    torch.cuda.synchronize()
+    assert r.meta.numel() == 0
+
+
+def test_status_strings_follow_reference_errors(ctx):
+    from capsule_amd import packets
+
+    pk = json.loads((GOLD / "reference_packets.json").read_text())
+    frames = [bytes.fromhex(pk["IPV6_TCP_PACKET"]["hex"]), bytes.fromhex(pk["ARP4_PACKET"]["hex"]),
+              b"", bytes(10)]
+    b = packets.PacketBatch.from_frames(frames, DEV)
+    r = packets.parse(ctx, b, flags=N.F_ACCEPT_V4 | N.F_ACCEPT_UDP)
+    torch.cuda.synchronize()
+    assert r.error(0) == "not an IPv4 packet."
+    assert r.error(1) == "not an IPv4 packet."
+    assert r.error(2) == "BadOffset"
+    assert r.error(3) == "OutOfBuffer"
