@@ -12,8 +12,8 @@ __all__ = ["native", "synth", "packets"]
 
 def __getattr__(name):
     # `packets` needs torch; import it lazily so synth/native stay light.
-    if name == "packets":
-        from . import packets
+    if name in ("packets", "shards"):
+        import importlib
 
-        return packets
+        return importlib.import_module(f"{__name__}.{name}")
     raise AttributeError(name)

@@ -26,17 +26,31 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void *p, uint32_t bytes) {
                                            0x00020000);
 }
 
+// One dword at a 4-byte-aligned arena offset that may straddle the end of
+// the arena.  The buffer range check drops a whole dword that crosses
+// num_records, so the bytes still inside are fetched one by one.
+__device__ __forceinline__ uint32_t load4_tail(rsrc_t rs, uint32_t byte_off, uint32_t arena_len) {
+  if ((uint64_t)byte_off + 4u <= (uint64_t)arena_len)
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)byte_off, 0, 0);
+  uint32_t v = 0;
+  for (uint32_t b = 0; b < 3u; ++b)
+    if (byte_off + b < arena_len)
+      v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(byte_off + b), 0, 0) << (8u * b);
+  return v;
+}
+
 // 16 bytes at a 4-byte-aligned arena offset.  Near the end of the arena the
-// load is split into dwords so that each dword gets its own range check.
+// load is split so that bytes up to the last one are still returned (and
+// zeros past it).
 __device__ __forceinline__ u32x4 load16(rsrc_t rs, uint32_t byte_off, uint32_t arena_len) {
   if ((uint64_t)byte_off + 16u <= (uint64_t)arena_len) {
     return __builtin_amdgcn_raw_buffer_load_b128(rs, (int)byte_off, 0, 0);
   }
   u32x4 v;
-  v[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)byte_off, 0, 0);
-  v[1] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(byte_off + 4), 0, 0);
-  v[2] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(byte_off + 8), 0, 0);
-  v[3] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(byte_off + 12), 0, 0);
+  v[0] = load4_tail(rs, byte_off, arena_len);
+  v[1] = load4_tail(rs, byte_off + 4u, arena_len);
+  v[2] = load4_tail(rs, byte_off + 8u, arena_len);
+  v[3] = load4_tail(rs, byte_off + 12u, arena_len);
   return v;
 }
 

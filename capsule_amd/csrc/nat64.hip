@@ -264,8 +264,28 @@ __device__ __forceinline__ uint32_t out_dw(uint32_t k, int j, const uint32_t (&P
               out_dw_k<2>(j, P, H, port_be));
 }
 
-__device__ __forceinline__ void store16(rsrc_t ors, uint32_t out_base, uint32_t c, u32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(out_base + 16u * c), 0, 0);
+// Chunk c (output bytes [16c, 16c+16)) of a frame of `len` bytes at a
+// 4-byte-aligned output offset.  Bytes at or past `len` are never written, so
+// tightly packed output slots do not clobber each other.
+__device__ __forceinline__ void store16(rsrc_t ors, uint32_t out_base, uint32_t c, u32x4 v,
+                                        uint32_t len) {
+  const uint32_t o = out_base + 16u * c;
+  if (16u * c + 16u <= len) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)o, 0, 0);
+    return;
+  }
+#pragma unroll
+  for (uint32_t t = 0; t < 4u; ++t) {
+    const uint32_t b = 16u * c + 4u * t;
+    if (b + 4u <= len) {
+      __builtin_amdgcn_raw_buffer_store_b32(v[t], ors, (int)(o + 4u * t), 0, 0);
+    } else {
+      for (uint32_t k = 0; k < 3u; ++k)
+        if (b + k < len)
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[t] >> (8u * k)), ors,
+                                               (int)(o + 4u * t + k), 0, 0);
+    }
+  }
 }
 
 __device__ __forceinline__ void store16_bytes(uint8_t *p, uint32_t lim, u32x4 v) {
@@ -331,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void nat64_rewrite(Nat64Args a) {
       acc += (uint64_t)(d & m);
     }
     if (c < 3) {
-      if (aligned) store16(ors, out_base, c, o);
+      if (aligned) store16(ors, out_base, c, o, new_len);
       else store16_bytes(obytes + 16 * c, new_len - 16u * c, o);
     } else {
       chunk3 = o;
@@ -350,7 +370,7 @@ __global__ __launch_bounds__(kBlock) void nat64_rewrite(Nat64Args a) {
     o[3] = __builtin_amdgcn_alignbyte(q2[1], q2[0], sh);
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc += (uint64_t)(o[t] & end_mask((int)(4u * c) + t, new_len));
-    if (aligned) store16(ors, out_base, c, o);
+    if (aligned) store16(ors, out_base, c, o, new_len);
     else store16_bytes(obytes + 16u * c, new_len - 16u * c, o);
   }
   // TCP checksum with the v4 pseudo-header (checksum.rs:93-103).
@@ -364,7 +384,7 @@ __global__ __launch_bounds__(kBlock) void nat64_rewrite(Nat64Args a) {
 #pragma unroll
   for (int t = 0; t < 4; ++t)
     if ((uint32_t)t == cs_t) chunk3[t] |= swap16(tcp_c) << 16;
-  if (aligned) store16(ors, out_base, 3, chunk3);
+  if (aligned) store16(ors, out_base, 3, chunk3, new_len);
   else store16_bytes(obytes + 48, new_len - 48u, chunk3);
 
   a.out_len[i] = (uint16_t)new_len;

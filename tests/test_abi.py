@@ -73,3 +73,10 @@ def test_record_layout_matches_header():
                        ("src_port", 72), ("l4_checksum", 78), ("seq_no", 80), ("data_offset", 88),
                        ("urgent_pointer", 92)):
         assert dt.fields[field][1] == off, field
+
+
+def test_host_modules_import_without_gpu():
+    import capsule_amd
+    from capsule_amd import packets, shards  # noqa: F401
+
+    assert capsule_amd.packets is packets

@@ -136,3 +136,35 @@ def test_config4_full_size_properties(ctx):
     got = out[:, 34].astype(np.int64) * 256 + out[:, 35]
     assert (got == want).all()
     assert gw.size() == len(first) and gw.next_port() == (1025 + len(first)) & 0xFFFF
+
+
+def test_packed_output_slots_do_not_clobber(ctx):
+    """Output frames packed back to back (out_off = running sum of new
+    lengths, unaligned): the whole output arena must equal the oracle's, so
+    no lane writes past its own frame."""
+    from capsule_amd import packets
+
+    rng = np.random.default_rng(31)
+    frames = []
+    for i in range(4000):
+        L = int(rng.integers(75, 300))
+        fr = synth.build_frames(rng, 1, synth.V6_TCP, L, int(rng.integers(0, 3)), 1)[0]
+        frames.append(bytes(fr))
+    arena, off, ln = synth.pack_frames(frames, slot=64)
+    new_len = ln.astype(np.int64) - 20
+    out_off = np.zeros(len(ln), np.int64)
+    out_off[1:] = np.cumsum(new_len)[:-1]
+    out_off = (out_off + 3).astype(np.uint32)
+    size = int(out_off[-1] + new_len[-1]) + 5
+    pm = oracle_lib.PortMap()
+    o_out, o_len, o_disp, _ = pm.nat_6to4(arena, off, ln, out_off, size)
+    assert (o_disp == N.ACT).all()
+    gw = packets.Nat64Gateway(ctx, capacity_log2=14)
+    out_arena = torch.zeros(size, dtype=torch.uint8, device=DEV)
+    oo = torch.from_numpy(out_off.view(np.int32)).to(DEV)
+    gw.nat_6to4(packets.PacketBatch.from_numpy(arena, off, ln, DEV), out_arena=out_arena,
+                out_off=oo)
+    torch.cuda.synchronize()
+    g = out_arena.cpu().numpy()
+    bad = np.nonzero(g != o_out)[0]
+    assert not len(bad), f"output arena differs at {bad[:8]}"
