@@ -138,7 +138,6 @@ int cgpu_parse_batch(cgpu_ctx *ctx, const cgpu_batch *batch, uint32_t flags,
   if (int e = check_batch(batch)) return fail(e);
   if (batch->n == 0) return ok();
   if (!out->meta) return fail(CGPU_EINVAL);
-  if ((flags & (CGPU_F_CSUM_IP | CGPU_F_CSUM_L4)) && !out->csum) return fail(CGPU_EINVAL);
   if ((flags & CGPU_F_FLOW_HASH) && !out->flow_hash) return fail(CGPU_EINVAL);
   if ((flags & CGPU_F_ACCEPT_ALL) == 0) flags |= CGPU_F_ACCEPT_ALL;
   cgpu::ParseArgs a;

@@ -136,89 +136,103 @@ __device__ __forceinline__ uint64_t sum_abs(rsrc_t rs, uint32_t arena_len, uint3
 }
 
 // ---- SipHash-1-3, key (0, 0): Rust std DefaultHasher::new() ---------------
-struct Sip {
-  uint64_t v0, v1, v2, v3;
+// The 64-bit state words are kept as explicit 32-bit halves: a rotation by
+// b < 32 is two v_alignbit_b32, a rotation by 32 is a rename, an add is
+// v_add_co + v_addc.  (Letting the compiler see uint64_t produced 64-bit
+// shift pairs plus register-pair moves for every rotation.)
+struct W64 {
+  uint32_t lo, hi;
 };
 
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int b) {
-  return (x << b) | (x >> (64 - b));
+__device__ __forceinline__ W64 w64(uint64_t x) { return W64{(uint32_t)x, (uint32_t)(x >> 32)}; }
+
+__device__ __forceinline__ W64 add64(W64 a, W64 b) {
+  W64 r;
+  r.lo = a.lo + b.lo;
+  r.hi = a.hi + b.hi + (r.lo < a.lo ? 1u : 0u);
+  return r;
 }
 
+__device__ __forceinline__ W64 xor64(W64 a, W64 b) { return W64{a.lo ^ b.lo, a.hi ^ b.hi}; }
+
+template <int B>
+__device__ __forceinline__ W64 rotl64(W64 x) {
+  static_assert(B > 0 && B < 32, "rotation by 32 is a swap");
+  return W64{__builtin_amdgcn_alignbit(x.lo, x.hi, 32 - B),
+             __builtin_amdgcn_alignbit(x.hi, x.lo, 32 - B)};
+}
+
+__device__ __forceinline__ W64 swap32(W64 x) { return W64{x.hi, x.lo}; }
+
+struct Sip {
+  W64 v0, v1, v2, v3;
+};
+
 __device__ __forceinline__ void sip_round(Sip &s) {
-  s.v0 += s.v1;
-  s.v1 = rotl64(s.v1, 13);
-  s.v1 ^= s.v0;
-  s.v0 = rotl64(s.v0, 32);
-  s.v2 += s.v3;
-  s.v3 = rotl64(s.v3, 16);
-  s.v3 ^= s.v2;
-  s.v0 += s.v3;
-  s.v3 = rotl64(s.v3, 21);
-  s.v3 ^= s.v0;
-  s.v2 += s.v1;
-  s.v1 = rotl64(s.v1, 17);
-  s.v1 ^= s.v2;
-  s.v2 = rotl64(s.v2, 32);
+  s.v0 = add64(s.v0, s.v1);
+  s.v1 = xor64(rotl64<13>(s.v1), s.v0);
+  s.v0 = swap32(s.v0);
+  s.v2 = add64(s.v2, s.v3);
+  s.v3 = xor64(rotl64<16>(s.v3), s.v2);
+  s.v0 = add64(s.v0, s.v3);
+  s.v3 = xor64(rotl64<21>(s.v3), s.v0);
+  s.v2 = add64(s.v2, s.v1);
+  s.v1 = xor64(rotl64<17>(s.v1), s.v2);
+  s.v2 = swap32(s.v2);
 }
 
 __device__ __forceinline__ Sip sip_init() {
   Sip s;
-  s.v0 = 0x736f6d6570736575ull;
-  s.v1 = 0x646f72616e646f6dull;
-  s.v2 = 0x6c7967656e657261ull;
-  s.v3 = 0x7465646279746573ull;
+  s.v0 = w64(0x736f6d6570736575ull);
+  s.v1 = w64(0x646f72616e646f6dull);
+  s.v2 = w64(0x6c7967656e657261ull);
+  s.v3 = w64(0x7465646279746573ull);
   return s;
 }
 
-__device__ __forceinline__ void sip_block(Sip &s, uint64_t m) {
-  s.v3 ^= m;
+__device__ __forceinline__ void sip_block(Sip &s, W64 m) {
+  s.v3 = xor64(s.v3, m);
   sip_round(s);
-  s.v0 ^= m;
+  s.v0 = xor64(s.v0, m);
 }
 
-__device__ __forceinline__ uint64_t sip_finish(Sip &s, uint64_t b) {
+__device__ __forceinline__ uint64_t sip_finish(Sip &s, W64 b) {
   sip_block(s, b);
-  s.v2 ^= 0xffull;
+  s.v2.lo ^= 0xffu;
   sip_round(s);
   sip_round(s);
   sip_round(s);
-  return s.v0 ^ s.v1 ^ s.v2 ^ s.v3;
-}
-
-__device__ __forceinline__ uint64_t u64_of(uint32_t lo, uint32_t hi) {
-  return (uint64_t)lo | ((uint64_t)hi << 32);
+  const W64 r = xor64(xor64(s.v0, s.v1), xor64(s.v2, s.v3));
+  return (uint64_t)r.lo | ((uint64_t)r.hi << 32);
 }
 
 // Hash of Flow{src_ip, dst_ip, src_port, dst_port, protocol} as Rust 1.50
 // `#[derive(Hash)]` feeds it to DefaultHasher:
 //   v4: [0u64][src 4B][0u64][dst 4B][sport le16][dport le16][proto]  = 29 B
 //   v6: [1u64][16u64][src 16B][1u64][16u64][dst 16B][ports][proto]   = 69 B
-// Addresses are given as the little-endian dwords of their wire bytes.
-__device__ __forceinline__ uint64_t flow_hash_v4(uint32_t src, uint32_t dst, uint32_t sport,
-                                                 uint32_t dport, uint32_t proto) {
+// Addresses are the little-endian dwords of their wire bytes; sport/dport
+// are host-order values.  v4 and v6 share the first three compressions'
+// code (blocks 0,1,2 differ only in their words), so a wave that mixes the
+// families pays 5 extra compressions for its v6 lanes instead of a second
+// full hash.
+__device__ __forceinline__ uint64_t flow_hash(bool v6, const uint32_t (&src)[4],
+                                              const uint32_t (&dst)[4], uint32_t sport,
+                                              uint32_t dport, uint32_t proto) {
   Sip s = sip_init();
-  sip_block(s, 0ull);
-  sip_block(s, (uint64_t)src);
-  sip_block(s, (uint64_t)dst << 32);
-  const uint64_t b = (29ull << 56) | ((uint64_t)proto << 32) | ((uint64_t)dport << 16) |
-                     (uint64_t)sport;
-  return sip_finish(s, b);
-}
-
-__device__ __forceinline__ uint64_t flow_hash_v6(const uint32_t (&src)[4],
-                                                 const uint32_t (&dst)[4], uint32_t sport,
-                                                 uint32_t dport, uint32_t proto) {
-  Sip s = sip_init();
-  sip_block(s, 1ull);
-  sip_block(s, 16ull);
-  sip_block(s, u64_of(src[0], src[1]));
-  sip_block(s, u64_of(src[2], src[3]));
-  sip_block(s, 1ull);
-  sip_block(s, 16ull);
-  sip_block(s, u64_of(dst[0], dst[1]));
-  sip_block(s, u64_of(dst[2], dst[3]));
-  const uint64_t b = (69ull << 56) | ((uint64_t)proto << 32) | ((uint64_t)dport << 16) |
-                     (uint64_t)sport;
+  // block 0: v4 [disc 0] ; v6 [disc 1]
+  sip_block(s, W64{v6 ? 1u : 0u, 0u});
+  // block 1: v4 [src][disc lo 0] ; v6 [16u64]
+  sip_block(s, W64{v6 ? 16u : src[0], 0u});
+  // block 2: v4 [disc hi 0][dst] ; v6 [src 0..7]
+  sip_block(s, v6 ? W64{src[0], src[1]} : W64{0u, dst[0]});
+  if (v6) {
+    sip_block(s, W64{src[2], src[3]});
+    sip_block(s, W64{1u, 0u});
+    sip_block(s, W64{16u, 0u});
+    sip_block(s, W64{dst[0], dst[1]});
+    sip_block(s, W64{dst[2], dst[3]});
+  }
+  const W64 b{sport | (dport << 16), proto | ((v6 ? 69u : 29u) << 24)};
   return sip_finish(s, b);
 }
 

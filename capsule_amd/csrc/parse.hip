@@ -1,12 +1,18 @@
 // parse.hip — batched Ethernet -> IPv4/IPv6 -> UDP/TCP parse, Internet
 // checksums and 5-tuple flow hash on gfx950.
 //
-// One packet per lane.  Each lane pulls a 96-byte packet-relative window
-// into VGPRs (buffer_load_dwordx4 + v_alignbyte, so any arena offset works),
-// parses every header from registers, sums the L4 span from the same
-// registers and streams only the bytes beyond the window.  Outputs are SoA:
-// a u32 meta word, a u32 (ip_csum | l4_csum << 16), a u64 flow hash and an
-// optional 96-byte header record.
+// One packet per lane.  A wave whose packets all sit at dword-aligned offsets
+// well inside the arena (the normal case: packets in 64-byte slots) loads
+// its 96-byte windows with unconditional buffer_load_dwordx4s (the last two
+// only when some lane's packet is that long: a wave-uniform ballot), and
+// reads every header field straight out of the loaded dwords; a wave with a
+// misaligned packet or one near the end of the arena takes the general,
+// tail-safe loader.  The window is shifted by the VLAN tag depth only when
+// some lane has a tagged frame.  Checksums are exact integer sums of u16
+// words accumulated with v_sad_u16 over the same registers (bytes past the
+// window are streamed from memory); with a wave-uniform frame length the end
+// masks are scalar.  Outputs are SoA: u32 meta, optional u32 (ip_csum |
+// l4_csum << 16), u64 flow hash, optional 96-byte header record.
 //
 // Reference chain restated (file:line in /root/reference):
 //   Ethernet::try_parse        core/src/packets/ethernet.rs:279-300, 164-181, 253-261
@@ -27,11 +33,47 @@ namespace cgpu {
 
 namespace {
 
-constexpr int kWinDw = 24;  // 96-byte register window
 constexpr uint32_t kBlock = 256;
+constexpr int kWin = 24;        // packet-relative window dwords (96 B)
+constexpr uint32_t kQEnd = 88;  // normalized window bytes valid after a QinQ shift
 
 __device__ __forceinline__ uint32_t sel3(uint32_t k, uint32_t a, uint32_t b, uint32_t c) {
   return k == 0u ? a : (k == 1u ? b : c);
+}
+
+// (x & 0xffff) + (x >> 16) + acc in one v_sad_u16: exact sum of the two
+// little-endian u16 words of a dword.
+__device__ __forceinline__ uint32_t sad16(uint32_t x, uint32_t acc) {
+  return __builtin_amdgcn_sad_u16(x, 0u, acc);
+}
+
+// General window loader: any byte offset, tail-safe at the end of the arena
+// (only waves with a misaligned packet or one near the arena end run it).
+__device__ __forceinline__ void load_window_general(rsrc_t rs, uint32_t arena_len, uint32_t off,
+                                                    uint32_t len, uint32_t (&P)[kWin]) {
+  const uint32_t sh = off & 3u;
+  const uint32_t base = off - sh;
+  const uint32_t need = sh + (len < 96u ? len : 96u);
+  uint32_t D[kWin + 1];
+#pragma unroll
+  for (int j = 0; j < kWin + 1; ++j)
+    D[j] = (uint32_t)(4 * j) < need ? load4_tail(rs, base + 4u * j, arena_len) : 0u;
+#pragma unroll
+  for (int j = 0; j < kWin; ++j) P[j] = __builtin_amdgcn_alignbyte(D[j + 1], D[j], sh);
+}
+
+// Sum of normalized window dwords j in [J0, 22) restricted to bytes < wend.
+template <int J0>
+__device__ __forceinline__ uint32_t sum_to_end(const uint32_t (&Q)[kWin - 2], uint32_t wend,
+                                               uint32_t acc) {
+#pragma unroll
+  for (int j = J0; j < (int)(kQEnd / 4); ++j) {
+    const uint32_t lo = 4u * (uint32_t)j;
+    uint32_t m = 0xffffffffu;
+    if (wend < lo + 4u) m = wend <= lo ? 0u : (0xffffffffu >> (8u * (lo + 4u - wend)));
+    acc = sad16(Q[j] & m, acc);
+  }
+  return acc;
 }
 
 template <bool IPC, bool L4C, bool HASH, bool FIELDS>
@@ -42,39 +84,64 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
   const uint32_t off = a.off[i];
   const uint32_t len = a.len[i];
 
-  uint32_t P[kWinDw];
-  load_window<kWinDw>(rs, a.arena_len, off, len < 96u ? len : 96u, P);
+  // --- the packet-relative window P ---------------------------------------
+  uint32_t P[kWin];
+  const bool slow = (off & 3u) != 0u || (uint64_t)off + 96u > (uint64_t)a.arena_len;
+  if (__ballot(slow)) {
+    load_window_general(rs, a.arena_len, off, len, P);
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u * c), 0, 0);
+      P[4 * c] = v[0];
+      P[4 * c + 1] = v[1];
+      P[4 * c + 2] = v[2];
+      P[4 * c + 3] = v[3];
+    }
+#pragma unroll
+    for (int c = 4; c < 6; ++c) {
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (__ballot(len > 16u * c)) v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u * c), 0, 0);
+      P[4 * c] = v[0];
+      P[4 * c + 1] = v[1];
+      P[4 * c + 2] = v[2];
+      P[4 * c + 3] = v[3];
+    }
+  }
 
   // --- Ethernet: VLAN marker at bytes 12-13 (ethernet.rs:164-181) ---------
   const uint32_t marker = be16_lo(P[3]);
   const uint32_t k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
   const uint32_t eth_len = 14u + 4u * k;  // header_len (ethernet.rs:253-261)
-  const uint32_t ether_type = be16_lo(sel3(k, P[3], P[4], P[5]));
-
-  // L[j] = L3-relative dword j (packet bytes eth_len + 4j ...): realign by
-  // 2 bytes, then shift by k dwords for the VLAN tags.
-  uint32_t A[20];
+  // Q: the window with the VLAN tags squeezed out (ether_type in Q[3] low
+  // half, L3 at normalized byte 14).
+  uint32_t Q[kWin - 2];
+  Q[0] = P[0];
+  Q[1] = P[1];
+  Q[2] = P[2];
+  if (__ballot(k != 0u)) {
 #pragma unroll
-  for (int j = 0; j < 20; ++j) A[j] = __builtin_amdgcn_alignbyte(P[4 + j], P[3 + j], 2);
-  uint32_t L[18];
+    for (int j = 3; j < kWin - 2; ++j) Q[j] = sel3(k, P[j], P[j + 1], P[j + 2]);
+  } else {
 #pragma unroll
-  for (int j = 0; j < 18; ++j) L[j] = sel3(k, A[j], A[j + 1], A[j + 2]);
+    for (int j = 3; j < kWin - 2; ++j) Q[j] = P[j];
+  }
+  const uint32_t ether_type = be16_lo(Q[3]);
 
   // --- status: the first failing step of the reference chain --------------
-  uint32_t st = CGPU_PKT_OK;
-  uint32_t l3 = CGPU_L3_NONE, l4 = CGPU_L4_NONE;
-  bool eth_ok = false, l3_ok = false;
   const bool v4 = ether_type == 0x0800u && (a.accept & CGPU_F_ACCEPT_V4);
   const bool v6 = ether_type == 0x86ddu && (a.accept & CGPU_F_ACCEPT_V6);
   const uint32_t l3_len = v6 ? 40u : 20u;
-  const uint32_t proto = v6 ? ((L[1] >> 16) & 0xffu) : ((L[2] >> 8) & 0xffu);
+  const uint32_t proto = v6 ? (Q[5] & 0xffu) : (Q[5] >> 24);
   const bool udp = proto == 17u && (a.accept & CGPU_F_ACCEPT_UDP);
   const bool tcp = proto == 6u && (a.accept & CGPU_F_ACCEPT_TCP);
   const uint32_t l4_off = eth_len + l3_len;
   const uint32_t l4_len = udp ? 8u : 20u;
+  uint32_t st = CGPU_PKT_OK;
+  bool eth_ok = false, l3_ok = false;
   if (len == 0u) {
     st = CGPU_PKT_ETH_BAD_OFFSET;
-  } else if (len < eth_len) {  // covers len < 14 and len < header_len
+  } else if (len < eth_len) {  // covers len < 14 and len < header_len (:294-297)
     st = CGPU_PKT_ETH_OUT_OF_BUFFER;
   } else {
     eth_ok = true;
@@ -87,7 +154,6 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
       st = CGPU_PKT_L3_OUT_OF_BUFFER;
     } else {
       l3_ok = true;
-      l3 = v6 ? CGPU_L3_IPV6 : CGPU_L3_IPV4;
       if (!udp && !tcp) {
         const bool au = a.accept & CGPU_F_ACCEPT_UDP, at = a.accept & CGPU_F_ACCEPT_TCP;
         st = (au && at) ? CGPU_PKT_NOT_L4 : (au ? CGPU_PKT_NOT_UDP : CGPU_PKT_NOT_TCP);
@@ -95,17 +161,10 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
         st = CGPU_PKT_L4_BAD_OFFSET;
       } else if (l4_off + l4_len > len) {
         st = CGPU_PKT_L4_OUT_OF_BUFFER;
-      } else {
-        l4 = udp ? CGPU_L4_UDP : CGPU_L4_TCP;
       }
     }
   }
   const bool l4_ok = st == CGPU_PKT_OK;
-
-  // U[j] = L4-relative dword j.
-  uint32_t U[5];
-#pragma unroll
-  for (int j = 0; j < 5; ++j) U[j] = v6 ? L[10 + j] : L[5 + j];
 
   uint32_t meta = st;
   if (eth_ok) {
@@ -113,65 +172,76 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
     if (k == 1u) meta |= CGPU_META_DOT1Q;
     if (k == 2u) meta |= CGPU_META_QINQ;
   }
-  meta |= l3 << 16;
-  meta |= l4 << 18;
+  if (l3_ok) meta |= (v6 ? CGPU_L3_IPV6 : CGPU_L3_IPV4) << 16;
+  if (l4_ok) meta |= (udp ? CGPU_L4_UDP : CGPU_L4_TCP) << 18;
+
+  // L4 header dwords (L4 starts at normalized byte 34 for v4, 54 for v6)
+  uint32_t U[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+    U[j] = __builtin_amdgcn_alignbyte(v6 ? Q[14 + j] : Q[9 + j], v6 ? Q[13 + j] : Q[8 + j], 2);
 
   uint32_t ip_c = 0, l4_c = 0;
   if (IPC && l3_ok && !v6) {
-    // compute(0, header with checksum zeroed): LE residue, swap to BE order.
-    const uint64_t s = (uint64_t)L[0] + L[1] + (L[2] & 0xffffu) + L[3] + L[4];
-    ip_c = (~swap16(fold64(s))) & 0xffffu;
-    if (ip_c == be16_hi(L[2])) meta |= CGPU_META_IP_CSUM_OK;
+    // compute(0, 20-B header with the checksum zeroed) (v4.rs:322-333)
+    uint32_t s = sad16(Q[3] & 0xffff0000u, 0u);
+    s = sad16(Q[4], s);
+    s = sad16(Q[5], s);
+    s = sad16(Q[6] & 0xffff0000u, s);
+    s = sad16(Q[7], s);
+    s = sad16(Q[8] & 0xffffu, s);
+    ip_c = (~swap16(fold32(s))) & 0xffffu;
+    if (ip_c == swap16(Q[6] & 0xffffu)) meta |= CGPU_META_IP_CSUM_OK;
   }
   if (L4C && l4_ok) {
-    const uint32_t l4dw = v6 ? 10u : 5u;
-    const uint32_t end = len - eth_len;  // L3-relative end of the span
-    const uint32_t cs_dw = udp ? l4dw + 1u : l4dw + 4u;
-    const uint32_t cs_keep = udp ? 0x0000ffffu : 0xffff0000u;
-    uint64_t acc = 0;
-#pragma unroll
-    for (int j = 5; j < 18; ++j) {
-      uint32_t m = ((uint32_t)j >= l4dw) ? end_mask(j, end) : 0u;
-      if ((uint32_t)j == cs_dw) m &= cs_keep;
-      acc += (uint64_t)(L[j] & m);
-    }
-    if (len > eth_len + 72u) {  // span continues past the register window
-      uint32_t rt = fold64(sum_abs(rs, a.arena_len, off + eth_len + 72u, off + len));
-      if (off & 1u) rt = swap16(rt);  // absolute parity -> packet parity
-      acc += rt;
-    }
-    const uint32_t sum_be = swap16(fold64(acc));
-    const uint32_t span = (len - l4_off) & 0xffffu;
-    const uint32_t pr = udp ? 17u : 6u;
-    uint32_t ph;
-    if (v6) {
-      const uint64_t as = (uint64_t)L[2] + L[3] + L[4] + L[5] + L[6] + L[7] + L[8] + L[9];
-      ph = fold32(swap16(fold64(as)) + span + pr);
+    // pseudo-header addresses + span [l4, len) (udp.rs:204-219, tcp.rs:
+    // 462-477, checksum.rs:56-128) are one contiguous byte range: [26, len)
+    // for v4, [22, len) for v6; the stored checksum field is subtracted.
+    uint32_t s = sad16(v6 ? (Q[5] & 0xffff0000u) : 0u, 0u);
+    s = sad16(v6 ? Q[6] : (Q[6] & 0xffff0000u), s);
+    const uint32_t endn = len - 4u * k;  // normalized end of frame
+    const uint32_t wend = endn < kQEnd ? endn : kQEnd;
+    if (!__ballot(wend != __builtin_amdgcn_readfirstlane(wend))) {
+      s = sum_to_end<7>(Q, __builtin_amdgcn_readfirstlane(wend), s);  // scalar masks
     } else {
-      const uint32_t src = be32(L[3]), dst = be32(L[4]);
-      ph = fold32((src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu) + pr + span);
+      s = sum_to_end<7>(Q, wend, s);
     }
-    l4_c = (~fold32(ph + sum_be)) & 0xffffu;
+    const uint32_t stored_le = udp ? (v6 ? (Q[15] & 0xffffu) : (Q[10] & 0xffffu))
+                                   : (v6 ? (Q[17] >> 16) : (Q[12] >> 16));
+    s -= stored_le;
+    if (endn > kQEnd) {  // span continues past the window: stream it
+      const uint32_t from = off + kQEnd + 4u * k;
+      uint32_t rt = fold64(sum_abs(rs, a.arena_len, from, off + len));
+      if (off & 1u) rt = swap16(rt);  // absolute parity -> packet parity
+      s += rt;
+    }
+    const uint32_t span = (len - l4_off) & 0xffffu;
+    l4_c = (~fold32(swap16(fold32(s)) + span + (udp ? 17u : 6u))) & 0xffffu;
     if (udp && l4_c == 0u) l4_c = 0xffffu;  // udp.rs:137-140
-    const uint32_t stored = udp ? be16_hi(U[1]) : be16_lo(U[4]);
-    if (l4_c == stored) meta |= CGPU_META_L4_CSUM_OK;
+    if (l4_c == swap16(stored_le)) meta |= CGPU_META_L4_CSUM_OK;
   }
 
   a.meta[i] = meta;
-  if (IPC || L4C) a.csum[i] = ip_c | (l4_c << 16);
+  if ((IPC || L4C) && a.csum != nullptr) a.csum[i] = ip_c | (l4_c << 16);
+
+  // addresses as LE dwords of their wire bytes
+  uint32_t src[4], dst[4];
+  if (HASH || FIELDS) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      src[j] = __builtin_amdgcn_alignbyte(Q[6 + j], Q[5 + j], 2);   // v6: bytes 22..37
+      dst[j] = __builtin_amdgcn_alignbyte(Q[10 + j], Q[9 + j], 2);  // v6: bytes 38..53
+    }
+    if (!v6) {
+      src[0] = __builtin_amdgcn_alignbyte(Q[7], Q[6], 2);  // v4: bytes 26..29
+      dst[0] = __builtin_amdgcn_alignbyte(Q[8], Q[7], 2);  // v4: bytes 30..33
+    }
+  }
 
   if (HASH) {
     uint64_t h = 0;
-    if (l4_ok) {
-      const uint32_t sport = be16_lo(U[0]), dport = be16_hi(U[0]);
-      const uint32_t pr = udp ? 17u : 6u;  // layer constant (udp.rs:157, tcp.rs:415)
-      if (v6) {
-        const uint32_t s6[4] = {L[2], L[3], L[4], L[5]};
-        const uint32_t d6[4] = {L[6], L[7], L[8], L[9]};
-        h = flow_hash_v6(s6, d6, sport, dport, pr);
-      } else {
-        h = flow_hash_v4(L[3], L[4], sport, dport, pr);
-      }
+    if (l4_ok) {  // Udp::flow / Tcp::flow (udp.rs:151-159, tcp.rs:409-417)
+      h = flow_hash(v6, src, dst, be16_lo(U[0]), be16_hi(U[0]), udp ? 17u : 6u);
     }
     a.hash[i] = h;
   }
@@ -186,31 +256,31 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
       R[2] = P[2];
       R[3] = ether_type | (eth_len << 16) | (k << 24);
     }
-    if (l3_ok && !v6) {
-      const uint32_t vihl = L[0] & 0xffu, de = (L[0] >> 8) & 0xffu;
+    if (l3_ok && !v6) {  // accessors ip/v4.rs:164-357
+      const uint32_t vihl = (Q[3] >> 16) & 0xffu, de = Q[3] >> 24;
       R[4] = (vihl >> 4) | ((vihl & 0xfu) << 8) | ((de >> 2) << 16) | ((de & 3u) << 24);
-      R[5] = be16_hi(L[0]) | (be16_lo(L[1]) << 16);
-      const uint32_t ff = be16_hi(L[1]);
+      R[5] = be16_lo(Q[4]) | (be16_hi(Q[4]) << 16);
+      const uint32_t ff = be16_lo(Q[5]);
       const uint32_t fl = ((ff & 0x4000u) ? 1u : 0u) | ((ff & 0x2000u) ? 2u : 0u);
-      R[6] = fl | ((L[2] & 0xffu) << 8) | ((ff & 0x1fffu) << 16);
-      R[7] = ((L[2] >> 8) & 0xffu) | (be16_hi(L[2]) << 16);
-      R[10] = L[3];
-      R[14] = L[4];
+      R[6] = fl | (((Q[5] >> 16) & 0xffu) << 8) | ((ff & 0x1fffu) << 16);
+      R[7] = (Q[5] >> 24) | (be16_lo(Q[6]) << 16);
+      R[10] = src[0];
+      R[14] = dst[0];
     }
-    if (l3_ok && v6) {
-      const uint32_t w = be32(L[0]);
+    if (l3_ok && v6) {  // accessors ip/v6/mod.rs:116-209
+      const uint32_t w = be32(__builtin_amdgcn_alignbyte(Q[4], Q[3], 2));
       R[4] = (w >> 28) | (((w & 0x0fc00000u) >> 22) << 16) | (((w & 0x00300000u) >> 20) << 24);
-      R[5] = be16_lo(L[1]);
-      R[6] = (L[1] >> 24) << 8;
-      R[7] = (L[1] >> 16) & 0xffu;
+      R[5] = be16_hi(Q[4]);
+      R[6] = ((Q[5] >> 8) & 0xffu) << 8;
+      R[7] = Q[5] & 0xffu;
       R[8] = w & 0xfffffu;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        R[10 + j] = L[2 + j];
-        R[14 + j] = L[6 + j];
+        R[10 + j] = src[j];
+        R[14 + j] = dst[j];
       }
     }
-    if (l4_ok) {
+    if (l4_ok) {  // udp.rs:90-128, tcp.rs:139-405
       R[18] = be16_lo(U[0]) | (be16_hi(U[0]) << 16);
       if (udp) {
         R[19] = be16_lo(U[1]) | (be16_hi(U[1]) << 16);
@@ -223,11 +293,11 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
         R[23] = be16_hi(U[4]);
       }
     }
-    u32x4 *dst = reinterpret_cast<u32x4 *>(a.fields + i);
+    u32x4 *out = reinterpret_cast<u32x4 *>(a.fields + i);
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       u32x4 v = {R[4 * q], R[4 * q + 1], R[4 * q + 2], R[4 * q + 3]};
-      dst[q] = v;
+      out[q] = v;
     }
   }
 }

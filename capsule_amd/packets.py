@@ -154,11 +154,14 @@ def parse_flags(accept=N.F_ACCEPT_ALL, csum_ip=True, csum_l4=True, flow_hash=Tru
 
 
 class ParseBuffers:
-    """Preallocated outputs for repeated `parse` calls on same-sized bursts."""
+    """Preallocated outputs for repeated `parse` calls on same-sized bursts.
 
-    def __init__(self, n, device, fields=False):
+    csum=False: verify-only checksums (the CSUM_OK bits of meta are still
+    set; the computed values are not stored)."""
+
+    def __init__(self, n, device, fields=False, csum=True):
         self.meta = torch.empty(n, dtype=torch.int32, device=device)
-        self.csum = torch.empty(n, dtype=torch.int32, device=device)
+        self.csum = torch.empty(n, dtype=torch.int32, device=device) if csum else None
         self.flow_hash = torch.empty(n, dtype=torch.int64, device=device)
         self.fields = (torch.empty((n, N.HDR_RECORD_SIZE), dtype=torch.uint8, device=device)
                        if fields else None)
@@ -179,14 +182,15 @@ def parse(ctx, batch, flags=None, fields=False, out=None, stream=None):
         out = ParseBuffers(n, batch.arena.device, fields)
     po = N.ParseOut()
     po.meta = out.meta.data_ptr()
-    po.csum = out.csum.data_ptr()
+    po.csum = out.csum.data_ptr() if out.csum is not None else None
     po.flow_hash = out.flow_hash.data_ptr()
     po.fields = out.fields.data_ptr() if (fields and out.fields is not None) else None
     cb = batch.cbatch()
     rc = N.lib().cgpu_parse_batch(ctx.handle, ctypes.byref(cb), flags, ctypes.byref(po),
                                   _stream_handle(stream))
     N.check(rc, "cgpu_parse_batch")
-    return ParsedBatch(out.meta[:n], out.csum[:n], out.flow_hash[:n],
+    return ParsedBatch(out.meta[:n], out.csum[:n] if out.csum is not None else None,
+                       out.flow_hash[:n],
                        out.fields[:n] if (fields and out.fields is not None) else None)
 
 

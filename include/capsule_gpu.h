@@ -152,7 +152,8 @@ typedef struct cgpu_hdr_record {
 /* Outputs of cgpu_parse_batch, all device pointers with n entries.       */
 typedef struct cgpu_parse_out {
   uint32_t *meta;       /* required                                          */
-  uint32_t *csum;       /* ip_calc | l4_calc << 16; required with CSUM flags  */
+  uint32_t *csum;       /* ip_calc | l4_calc << 16, or NULL: verify only (the
+                         * CSUM_OK bits of meta are set either way)          */
   uint64_t *flow_hash;  /* required with CGPU_F_FLOW_HASH                     */
   cgpu_hdr_record *fields; /* optional (NULL = skip field extraction)        */
 } cgpu_parse_out;

@@ -147,7 +147,7 @@ def test_packed_output_slots_do_not_clobber(ctx):
     rng = np.random.default_rng(31)
     frames = []
     for i in range(4000):
-        L = int(rng.integers(75, 300))
+        L = int(rng.integers(90, 300))
         fr = synth.build_frames(rng, 1, synth.V6_TCP, L, int(rng.integers(0, 3)), 1)[0]
         frames.append(bytes(fr))
     arena, off, ln = synth.pack_frames(frames, slot=64)

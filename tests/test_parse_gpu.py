@@ -180,3 +180,16 @@ def test_status_strings_follow_reference_errors(ctx):
     assert r.error(1) == "not an IPv4 packet."
     assert r.error(2) == "BadOffset"
     assert r.error(3) == "OutOfBuffer"
+
+
+def test_verify_only_mode_sets_same_meta(ctx):
+    """csum=NULL (verify only) gives the same meta word as storing the values."""
+    from capsule_amd import packets
+
+    arena, off, ln = synth.fuzz(3000, seed=55)
+    b = packets.PacketBatch.from_numpy(arena, off, ln, DEV)
+    r1 = packets.parse(ctx, b, flags=ALL)
+    r2 = packets.parse(ctx, b, flags=ALL, out=packets.ParseBuffers(b.n, DEV, csum=False))
+    torch.cuda.synchronize()
+    assert r2.csum is None
+    assert torch.equal(r1.meta, r2.meta) and torch.equal(r1.flow_hash, r2.flow_hash)

@@ -1,0 +1,153 @@
+// microbench.hip — roofline calibration and ablations for the parse kernel.
+//
+//   stream_read   : coalesced dwordx4 grid-stride read of the arena (the
+//                   achievable HBM read bandwidth on this box)
+//   aos_window    : one lane per packet loads its own 64 B (the parse
+//                   kernel's access pattern with no compute), writes 4 B
+//   parse[flags]  : cgpu_parse_batch through the C ABI with feature subsets
+//
+// Each case rotates over R copies of the batch (> 256 MiB Infinity Cache)
+// and reports mean device time per launch from hipEvents around a run of
+// back-to-back launches.  Build: make -C tools ; run: tools/microbench
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "capsule_gpu.h"
+
+#define CK(x)                                                                 \
+  do {                                                                        \
+    hipError_t e_ = (x);                                                      \
+    if (e_ != hipSuccess) {                                                   \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(2);                                                                \
+    }                                                                         \
+  } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void stream_read(const u32x4 *p, size_t n16, uint32_t *out) {
+  uint32_t acc = 0;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256ull) {
+    u32x4 v = __builtin_nontemporal_load(p + i);
+    acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+  }
+  if (acc == 0x9e3779b9u) out[blockIdx.x] = acc;  // practically never: keeps the loads
+}
+
+__global__ __launch_bounds__(256) void aos_window(const uint8_t *arena, const uint32_t *off,
+                                                  uint32_t n, uint32_t *out) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const u32x4 *q = reinterpret_cast<const u32x4 *>(arena + off[i]);
+  u32x4 a = q[0], b = q[1], c = q[2], d = q[3];
+  u32x4 s = a + b + c + d;
+  out[i] = s[0] ^ s[1] ^ s[2] ^ s[3];
+}
+
+static uint32_t lcg(uint64_t &s) {
+  s = s * 6364136223846793005ull + 1442695040888963407ull;
+  return (uint32_t)(s >> 33);
+}
+
+int main(int argc, char **argv) {
+  const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : (1u << 20);
+  const int iters = argc > 2 ? atoi(argv[2]) : 400;
+  const uint32_t L = 64;
+  const size_t bytes = (size_t)n * L;
+  const int R = 8;
+  const char *filter = argc > 3 ? argv[3] : "";
+  // synthetic IPv4/UDP frames (checksums are not reconciled: timing only)
+  std::vector<uint8_t> h(bytes);
+  uint64_t s = 12345;
+  for (size_t i = 0; i < bytes; ++i) h[i] = (uint8_t)lcg(s);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint8_t *f = &h[(size_t)i * L];
+    f[12] = 0x08; f[13] = 0x00; f[14] = 0x45; f[23] = 17;
+  }
+  std::vector<uint32_t> ho(n);
+  std::vector<uint16_t> hl(n, (uint16_t)L);
+  for (uint32_t i = 0; i < n; ++i) ho[i] = i * L;
+  uint8_t *arena[R];
+  uint32_t *off[R];
+  uint16_t *len[R];
+  for (int r = 0; r < R; ++r) {
+    CK(hipMalloc(&arena[r], bytes));
+    CK(hipMalloc(&off[r], 4ull * n));
+    CK(hipMalloc(&len[r], 2ull * n));
+    CK(hipMemcpy(arena[r], h.data(), bytes, hipMemcpyHostToDevice));
+    CK(hipMemcpy(off[r], ho.data(), 4ull * n, hipMemcpyHostToDevice));
+    CK(hipMemcpy(len[r], hl.data(), 2ull * n, hipMemcpyHostToDevice));
+  }
+  uint32_t *meta, *csum, *scratch;
+  uint64_t *hash;
+  CK(hipMalloc(&meta, 4ull * n));
+  CK(hipMalloc(&csum, 4ull * n));
+  CK(hipMalloc(&hash, 8ull * n));
+  CK(hipMalloc(&scratch, 4ull * n + 4096 * 4));
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  cgpu_ctx *ctx;
+  if (cgpu_ctx_create(0, &ctx)) { fprintf(stderr, "ctx\n"); return 2; }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+
+  auto time_it = [&](const char *name, double algo_bytes, auto &&launch) {
+    if (filter[0] && !strstr(name, filter)) return;
+    for (int w = 0; w < 20; ++w) launch(w % R);
+    CK(hipStreamSynchronize(st));
+    CK(hipEventRecord(e0, st));
+    for (int k = 0; k < iters; ++k) launch(k % R);
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1e3 * ms / iters;
+    printf("{\"case\": \"%s\", \"us\": %.3f, \"GBps\": %.1f, \"Mpps\": %.1f}\n", name, us,
+           algo_bytes / (us * 1e-6) / 1e9, n / us);
+    fflush(stdout);
+  };
+
+  const double algo = (double)bytes + 6.0 * n;
+  for (int grid : {1024, 2048, 4096, 8192}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "stream_read_grid%d", grid);
+    time_it(nm, (double)bytes, [&](int r) {
+      hipLaunchKernelGGL(stream_read, dim3(grid), dim3(256), 0, st, (const u32x4 *)arena[r],
+                         bytes / 16, scratch);
+    });
+  }
+  time_it("aos_window64", algo - 2.0 * n, [&](int r) {
+    hipLaunchKernelGGL(aos_window, dim3((n + 255) / 256), dim3(256), 0, st, arena[r], off[r], n,
+                       scratch);
+  });
+  struct {
+    const char *name;
+    uint32_t flags;
+    bool csum_out;
+  } cases[] = {
+      {"parse_only", CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_UDP, false},
+      {"parse_csum", CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_UDP | CGPU_F_CSUM_IP | CGPU_F_CSUM_L4, true},
+      {"parse_hash", CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_UDP | CGPU_F_FLOW_HASH, false},
+      {"parse_csum_hash",
+       CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_UDP | CGPU_F_CSUM_IP | CGPU_F_CSUM_L4 | CGPU_F_FLOW_HASH,
+       true},
+      {"parse_verify_hash",
+       CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_UDP | CGPU_F_CSUM_IP | CGPU_F_CSUM_L4 | CGPU_F_FLOW_HASH,
+       false},
+  };
+  for (auto &c : cases) {
+    time_it(c.name, algo, [&](int r) {
+      cgpu_batch b = {arena[r], bytes, off[r], len[r], n};
+      cgpu_parse_out o = {meta, c.csum_out ? csum : nullptr, hash, nullptr};
+      if (cgpu_parse_batch(ctx, &b, c.flags, &o, st)) { fprintf(stderr, "parse\n"); exit(2); }
+    });
+  }
+  cgpu_ctx_destroy(ctx);
+  return 0;
+}
