@@ -197,24 +197,32 @@ def main():
     torch.cuda.synchronize(dev)
 
     step = [0]
+    # HIP events on the launch stream bracket the K launches of the timed
+    # region: their span / K is the average device time per launch (kernel
+    # plus the back-to-back dispatch gap), without per-launch event overhead.
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def one():
+        if step[0] == args.warmup:
+            ev0.record(stream)
         launch(step[0])
         step[0] += 1
+        if step[0] == args.warmup + args.steps:
+            ev1.record(stream)
 
+    step[0] = args.warmup
     elapsed = g.timed(one, args.steps, sync=lambda: torch.cuda.synchronize(dev))
-
-    # per-launch kernel time with HIP events on the launch stream (separate pass
-    # so the events do not perturb the timed region)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(min(args.steps, 200))]
-    for k, (a, b) in enumerate(ev):
-        a.record(stream)
-        launch(k)
-        b.record(stream)
-    torch.cuda.synchronize(dev)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     achieved = w["algo_bytes"] / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = ROOT / "profiles" / f"pmc_{args.config}.json"
+    if pmc.exists():  # PMC HBM bytes of this exact kernel source (scripts/summarize_prof.py)
+        sys.path.insert(0, str(ROOT / "scripts"))
+        from summarize_prof import source_hash
+
+        p = json.loads(pmc.read_text())
+        if p.get("src_hash") == source_hash() and "traffic_bytes" in p:
+            traffic = int(p["traffic_bytes"])
 
     total_pkts = g.sum(n * args.steps)
     value = total_pkts / elapsed / 1e6
@@ -237,7 +245,7 @@ def main():
                    "parallelism": f"{g.world} independent RX-queue shards (no collective)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "kernel_us": round(kern_ms * 1e3, 3),
+                     "traffic": traffic, "kernel_us": round(kern_ms * 1e3, 3),
                      "algo_bytes_per_launch": w["algo_bytes"],
                      "mean_frac_over_ranks": round(frac_all, 4)},
     }
