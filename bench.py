@@ -180,17 +180,22 @@ def main():
         # checksum verify: CSUM_OK bits in meta, computed values not stored
         outs = [packets.ParseBuffers(n, dev, csum=False) for _ in range(2)]
 
+        launchers = [packets.ParseLauncher(ctx, batches[k % copies], outs[k & 1], w["flags"],
+                                           stream) for k in range(2 * copies)]
+
         def launch(k):
-            packets.parse(ctx, batches[k % copies], flags=w["flags"], out=outs[k & 1],
-                          stream=stream)
+            launchers[k % (2 * copies)]()
     else:
         gw = packets.Nat64Gateway(ctx, capacity_log2=17)
         nat_out = [(torch.empty_like(b.arena), b.off, torch.empty(n, dtype=torch.int16, device=dev),
                     torch.empty(n, dtype=torch.uint8, device=dev),
                     torch.empty(n, dtype=torch.uint8, device=dev)) for b in batches[:2]]
 
+        launchers = [packets.Nat64Launcher(gw, batches[k % copies], nat_out[k & 1], stream)
+                     for k in range(2 * copies)]
+
         def launch(k):
-            gw.nat_6to4(batches[k % copies], stream=stream, out=nat_out[k & 1])
+            launchers[k % (2 * copies)]()
 
     for k in range(args.warmup):
         launch(k)

@@ -53,6 +53,8 @@ struct cgpu_portmap {
   // per-call scratch
   uint32_t *pkt_slot = nullptr;
   uint32_t *block_sums = nullptr;
+  void *rec_h = nullptr;  // K1 -> K5 header records
+  void *rec_b = nullptr;
   uint32_t scratch_n = 0;
 };
 
@@ -325,9 +327,14 @@ int cgpu_nat64_6to4(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8
     pm->scratch_n = 0;
     const size_t nb = cgpu::nat64_num_blocks(in->n) + 1;
     void *m = nullptr;
-    if (hipMalloc(&m, 4ull * in->n + 4ull * nb + 256) != hipSuccess) return fail(CGPU_ENOMEM);
+    const size_t o_sums = align_up(4ull * in->n, 256);
+    const size_t o_rech = o_sums + align_up(4ull * nb, 256);
+    const size_t o_recb = o_rech + align_up(16ull * in->n, 256);
+    if (hipMalloc(&m, o_recb + 8ull * in->n + 256) != hipSuccess) return fail(CGPU_ENOMEM);
     pm->pkt_slot = (uint32_t *)m;
-    pm->block_sums = (uint32_t *)((uint8_t *)m + align_up(4ull * in->n, 256));
+    pm->block_sums = (uint32_t *)((uint8_t *)m + o_sums);
+    pm->rec_h = (uint8_t *)m + o_rech;
+    pm->rec_b = (uint8_t *)m + o_recb;
     pm->scratch_n = in->n;
   }
   cgpu::Nat64Args a;
@@ -344,6 +351,8 @@ int cgpu_nat64_6to4(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8
   a.status = status;
   a.pkt_slot = pm->pkt_slot;
   a.block_sums = pm->block_sums;
+  a.rec_h = (cgpu::u32x4 *)pm->rec_h;
+  a.rec_b = (uint2 *)pm->rec_b;
   a.pm = pm->dev;
   hipError_t e = cgpu::launch_nat64_6to4(a, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e);

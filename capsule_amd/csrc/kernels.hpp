@@ -9,6 +9,8 @@
 
 namespace cgpu {
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 struct ParseArgs {
   const uint8_t *arena;
   uint32_t arena_len;
@@ -55,6 +57,8 @@ struct Nat64Args {
   uint8_t *status;
   uint32_t *pkt_slot;    // scratch [n]: table slot (or 0xffffffff)
   uint32_t *block_sums;  // scratch [nblocks + 1]
+  u32x4 *rec_h;          // scratch [n]: new IPv4 header dwords 0..3 (K1 -> K5)
+  uint2 *rec_b;          // scratch [n]: header dword 4, eth_len | k << 8 | new_len << 16
   PortMapDev pm;
 };
 

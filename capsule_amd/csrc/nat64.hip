@@ -9,17 +9,22 @@
 // Ipv4::reconcile (ip/v4.rs:486-489).
 //
 // The reference assigns gateway ports from a global AtomicU16 (first 1025)
-// in first-seen order of (v6 src, tcp src port).  The batch reproduces that
+// in first-seen order of (v6 src, tcp src port).  A batch reproduces that
 // order exactly:
-//   K1 probe   : parse, classify (Act / Drop / Abort), insert-or-find the key
-//                in an open-addressing table; atomicMin the packet index
-//                into the slot so each new key knows its first packet.
-//   K2 count   : per-block count of "first packet of a new key".
-//   K3 scan    : exclusive scan of the block counts (one workgroup) and the
-//                NEXT_PORT update, all on the device.
-//   K4 assign  : in-block ballot scan -> ordinal -> port = base + ordinal.
-//   K5 rewrite : build the IPv4 frame, TCP + IPv4 checksums, write it, and
-//                commit new keys to the persistent table.
+//   K1 probe   : one lane per frame.  Classify (Act / Drop / Abort), look the
+//                key up in an open-addressing table (plain loads for keys
+//                committed by earlier batches; atomicCAS claims an empty slot,
+//                atomicMin records the first packet index of a new key), and
+//                write the frame's new IPv4 header (it does not depend on the
+//                port) to a 24-byte record.
+//   K2 count   : per-workgroup count of "first packet of a new key".
+//   K3 scan    : exclusive scan of the counts (one workgroup) + NEXT_PORT.
+//   K4 assign  : ballot/popcount prefix -> ordinal -> port = base + ordinal.
+//   K5 rewrite : sixteen lanes (one DPP row) per frame.  Lane g builds output
+//                bytes [16c, 16c + 16), c = 16q + g, from coalesced loads of
+//                the shifted input, sums its share of the TCP span with
+//                v_sad_u16, the row reduces it, and the lane holding the TCP
+//                checksum field stores last; then the key is committed.
 // Kernel boundaries are the only cross-workgroup hand-offs besides the
 // device-scope atomics on slot_ref / slot_min.
 #include "capsule_gpu.h"
@@ -31,6 +36,7 @@ namespace cgpu {
 namespace {
 
 constexpr uint32_t kBlock = 256;
+constexpr uint32_t kGroup = 16;  // lanes per frame in K5 (one DPP row)
 constexpr uint32_t kNoSlot = 0xffffffffu;
 constexpr uint32_t kFirstBit = 0x80000000u;  // pkt_slot: first packet of a new key
 constexpr uint32_t kV4Addr = 0x017100cbu;    // 203.0.113.1 as LE dword of wire bytes
@@ -38,6 +44,10 @@ constexpr uint32_t kDataRoom = 2048u;        // RTE_MBUF_DEFAULT_DATAROOM
 
 __device__ __forceinline__ uint32_t sel3(uint32_t k, uint32_t a, uint32_t b, uint32_t c) {
   return k == 0u ? a : (k == 1u ? b : c);
+}
+
+__device__ __forceinline__ uint32_t sad16(uint32_t x, uint32_t acc) {
+  return __builtin_amdgcn_sad_u16(x, 0u, acc);
 }
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int b) {
@@ -59,31 +69,56 @@ __device__ __forceinline__ uint32_t key_hash(const uint32_t (&key)[5]) {
   return h;
 }
 
+// Byte mask of dword [lo, lo+4) restricted to [s, e).
+__device__ __forceinline__ uint32_t range_mask(uint32_t lo, uint32_t s, uint32_t e) {
+  uint32_t m = 0xffffffffu;
+  if (s > lo) m = s >= lo + 4u ? 0u : (0xffffffffu << (8u * (s - lo)));
+  if (e < lo + 4u) m &= e <= lo ? 0u : (0xffffffffu >> (8u * (lo + 4u - e)));
+  return m;
+}
+
 // Classification of one input frame by the reference nat_6to4 control flow.
 struct V6 {
-  uint32_t k, eth_len, len;
+  uint32_t k, eth_len;
   uint32_t disp, st;
-  uint32_t L[18];  // L3-relative dwords (v6 header at 0..9, TCP at 10..14)
+  uint32_t L[11];  // L3-relative dwords: v6 header 0..9, TCP source port in L[10] lo
 };
 
-template <int NW>
+// Frame-relative dwords 0..19 (80 B) -> V6.  Fast path: dword-aligned frames
+// well inside the arena (wave-uniform), otherwise the tail-safe loader.
 __device__ __forceinline__ void classify(rsrc_t rs, uint32_t arena_len, uint32_t off,
-                                         uint32_t len, V6 &v, uint32_t (&P)[NW]) {
-  load_window<NW>(rs, arena_len, off, len < 4u * NW ? len : 4u * NW, P);
+                                         uint32_t len, V6 &v) {
+  constexpr int NW = 20;
+  uint32_t P[NW];
+  const bool slow = (off & 3u) != 0u || (uint64_t)off + 80u > (uint64_t)arena_len;
+  if (__ballot(slow)) {
+    const uint32_t sh = off & 3u, base = off - sh;
+    const uint32_t need = sh + (len < 80u ? len : 80u);
+    uint32_t D[NW + 1];
+#pragma unroll
+    for (int j = 0; j < NW + 1; ++j)
+      D[j] = (uint32_t)(4 * j) < need ? load4_tail(rs, base + 4u * j, arena_len) : 0u;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) P[j] = __builtin_amdgcn_alignbyte(D[j + 1], D[j], sh);
+  } else {
+#pragma unroll
+    for (int c = 0; c < NW / 4; ++c) {
+      const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u * c), 0, 0);
+      P[4 * c] = q[0];
+      P[4 * c + 1] = q[1];
+      P[4 * c + 2] = q[2];
+      P[4 * c + 3] = q[3];
+    }
+  }
   const uint32_t marker = be16_lo(P[3]);
   v.k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
   v.eth_len = 14u + 4u * v.k;
-  v.len = len;
   const uint32_t et = be16_lo(sel3(v.k, P[3], P[4], P[5]));
-  constexpr int NA = NW - 4;
-  uint32_t A[NA];
+  uint32_t A[13];
 #pragma unroll
-  for (int j = 0; j < NA; ++j) A[j] = __builtin_amdgcn_alignbyte(P[4 + j], P[3 + j], 2);
+  for (int j = 0; j < 13; ++j) A[j] = __builtin_amdgcn_alignbyte(P[4 + j], P[3 + j], 2);
 #pragma unroll
-  for (int j = 0; j < 18; ++j) {
-    if (j + 2 < NA) v.L[j] = sel3(v.k, A[j], A[j + 1], A[j + 2]);
-    else v.L[j] = 0u;
-  }
+  for (int j = 0; j < 11; ++j) v.L[j] = sel3(v.k, A[j], A[j + 1], A[j + 2]);
   v.disp = CGPU_ABORT;
   // packet.parse::<Ethernet>()? (ethernet.rs:279-300)
   if (len == 0u) { v.st = CGPU_PKT_ETH_BAD_OFFSET; return; }
@@ -122,24 +157,36 @@ __device__ __forceinline__ bool key_eq(const uint32_t (&a)[5], const uint32_t (&
   return a[0] == b[0] && a[1] == b[1] && a[2] == b[2] && a[3] == b[3] && a[4] == b[4];
 }
 
-// ---- K1: classify + probe --------------------------------------------------
+// ---- K1: classify + probe + header record -----------------------------------
 __global__ __launch_bounds__(kBlock) void nat64_probe(Nat64Args a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= a.n) return;
+  const bool valid = i < a.n;
   const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
+  const uint32_t off = valid ? a.off[i] : 0u, len = valid ? (uint32_t)a.len[i] : 0u;
   V6 v;
-  uint32_t P[20];
-  classify<20>(rs, a.arena_len, a.off[i], a.len[i], v, P);
+  classify(rs, a.arena_len, off, len, v);
+  if (!valid) return;
   uint32_t slot = kNoSlot;
   if (v.disp == CGPU_ACT) {
     uint32_t key[5];
     make_key(v, key);
     uint32_t h = key_hash(key) & a.pm.cap_mask;
     for (uint32_t probe = 0; probe <= a.pm.cap_mask; ++probe) {
-      const uint32_t ref = atomicCAS(&a.pm.slot_ref[h], 0u, i + 1u);
-      bool match;
+      // Keys committed by earlier batches are matched with plain loads; an
+      // empty slot is claimed with a CAS.  refs only ever go 0 -> (i + 1)
+      // -> kPersist, so a stale 0 just leads to the CAS.
+      uint32_t ref = a.pm.slot_ref[h];
+      bool claimed = false;
       if (ref == 0u) {
-        match = true;  // claimed an empty slot: this packet represents the key
+        ref = atomicCAS(&a.pm.slot_ref[h], 0u, i + 1u);
+        claimed = ref == 0u;
+      }
+      bool match;
+      if (claimed) {
+        match = true;  // this packet represents the key: publish the key words
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a.pm.key_src[4u * h + j] = key[j];
+        a.pm.key_port[h] = key[4];
       } else if (ref & kPersist) {
         uint32_t other[5];
 #pragma unroll
@@ -147,11 +194,12 @@ __global__ __launch_bounds__(kBlock) void nat64_probe(Nat64Args a) {
         other[4] = a.pm.key_port[h];
         match = key_eq(key, other);
       } else {
-        // batch-local entry: compare against the representative's own bytes
+        // a key first seen in this batch: compare with the representative
+        // frame's own bytes (immutable input), never with the table words
+        // its claimer may still be writing.
         const uint32_t rep = ref - 1u;
         V6 rv;
-        uint32_t RP[20];
-        classify<20>(rs, a.arena_len, a.off[rep], a.len[rep], rv, RP);
+        classify(rs, a.arena_len, a.off[rep], a.len[rep], rv);
         uint32_t other[5];
         make_key(rv, other);
         match = key_eq(key, other);
@@ -166,6 +214,26 @@ __global__ __launch_bounds__(kBlock) void nat64_probe(Nat64Args a) {
     if (slot == kNoSlot) {
       v.disp = CGPU_ABORT;
       v.st = CGPU_PKT_TABLE_FULL;
+    } else {
+      // The pushed IPv4 header (v4.rs:594-609) with the setters of main.rs:
+      // 133-138 and Ipv4::reconcile (v4.rs:486-489) already applied.
+      const uint32_t w = be32(v.L[0]);
+      const uint32_t dscp = (w & 0x0fc00000u) >> 22, ecn = (w & 0x00300000u) >> 20;
+      const uint32_t ttl = ((v.L[1] >> 24) - 1u) & 0xffu;  // hop_limit - 1 (u8, wrapping)
+      const uint32_t dscp_ecn = (((dscp << 2) & 0xfcu) | (ecn & 0x3u)) & 0xffu;
+      const uint32_t new_len = len - 20u;
+      uint32_t H[5];
+      H[0] = 0x45u | (dscp_ecn << 8) | (swap16((new_len - v.eth_len) & 0xffffu) << 16);
+      H[1] = 0u;               // identification 0, flags/fragment 0
+      H[2] = ttl | (6u << 8);  // protocol = next_header (6)
+      H[3] = kV4Addr;          // V4_ADDR (main.rs:35)
+      H[4] = v.L[9];           // map6to4(dst): low 32 bits (main.rs:79-83)
+      const uint32_t ip_c =
+          (~swap16(fold64((uint64_t)H[0] + H[1] + H[2] + H[3] + H[4]))) & 0xffffu;
+      H[2] |= swap16(ip_c) << 16;
+      const u32x4 hv = {H[0], H[1], H[2], H[3]};
+      a.rec_h[i] = hv;
+      a.rec_b[i] = make_uint2(H[4], v.eth_len | (v.k << 8) | (new_len << 16));
     }
   }
   a.pkt_slot[i] = slot;
@@ -198,8 +266,7 @@ __global__ __launch_bounds__(kScanBlock) void nat64_scan(Nat64Args a, uint32_t n
   for (uint32_t base = 0; base < nb; base += kScanBlock) {
     const uint32_t idx = base + threadIdx.x;
     const uint32_t v = idx < nb ? a.block_sums[idx] : 0u;
-    // inclusive wave scan
-    uint32_t x = v;
+    uint32_t x = v;  // inclusive wave scan
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(x, d, 64);
@@ -244,158 +311,127 @@ __global__ __launch_bounds__(kBlock) void nat64_assign(Nat64Args a) {
   }
 }
 
-// Output packet-relative dword j of the rewritten frame, for a fixed VLAN
-// depth KK (so every register index is static).  H = new IPv4 header dwords,
-// P = input window, pt = tcp src port dword patch.
-template <int KK>
-__device__ __forceinline__ uint32_t out_dw_k(int j, const uint32_t (&P)[24],
-                                             const uint32_t (&H)[5], uint32_t port_be) {
-  if (j < 3 + KK) return P[j];
-  if (j == 3 + KK) return __builtin_amdgcn_alignbyte(H[0], 0x00080000u, 2);  // ether_type 0x0800
-  if (j < 8 + KK) return __builtin_amdgcn_alignbyte(H[j - 3 - KK], H[j - 4 - KK], 2);
-  if (j == 8 + KK) return (H[4] >> 16) | (port_be << 16);  // dst tail | new tcp src port
-  if (j == 12 + KK) return P[j + 5] & 0x0000ffffu;          // tcp checksum zeroed
-  return P[j + 5];                                          // shifted TCP header/payload
+// 16 input bytes at any frame-relative byte position (tail-safe).
+__device__ __forceinline__ u32x4 load_in(rsrc_t rs, uint32_t arena_len, uint32_t abs_off,
+                                         bool aligned_wave) {
+  if (aligned_wave) return load16(rs, abs_off, arena_len);
+  const uint32_t sh = abs_off & 3u, base = abs_off - sh;
+  uint32_t D[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) D[j] = load4_tail(rs, base + 4u * j, arena_len);
+  u32x4 v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = __builtin_amdgcn_alignbyte(D[j + 1], D[j], sh);
+  return v;
 }
 
-__device__ __forceinline__ uint32_t out_dw(uint32_t k, int j, const uint32_t (&P)[24],
-                                           const uint32_t (&H)[5], uint32_t port_be) {
-  return sel3(k, out_dw_k<0>(j, P, H, port_be), out_dw_k<1>(j, P, H, port_be),
-              out_dw_k<2>(j, P, H, port_be));
-}
-
-// Chunk c (output bytes [16c, 16c+16)) of a frame of `len` bytes at a
-// 4-byte-aligned output offset.  Bytes at or past `len` are never written, so
-// tightly packed output slots do not clobber each other.
-__device__ __forceinline__ void store16(rsrc_t ors, uint32_t out_base, uint32_t c, u32x4 v,
-                                        uint32_t len) {
+// Store output bytes [16c, 16c+16) of a frame of `len` bytes at out_base;
+// bytes at or past `len` are never written (packed slots do not clobber).
+__device__ __forceinline__ void store_out(rsrc_t ors, uint8_t *out_arena, uint32_t out_base,
+                                          uint32_t c, u32x4 v, uint32_t len, bool aligned) {
   const uint32_t o = out_base + 16u * c;
-  if (16u * c + 16u <= len) {
+  if (aligned && 16u * c + 16u <= len) {
     __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)o, 0, 0);
     return;
   }
 #pragma unroll
   for (uint32_t t = 0; t < 4u; ++t) {
     const uint32_t b = 16u * c + 4u * t;
-    if (b + 4u <= len) {
+    if (aligned && b + 4u <= len) {
       __builtin_amdgcn_raw_buffer_store_b32(v[t], ors, (int)(o + 4u * t), 0, 0);
     } else {
-      for (uint32_t k = 0; k < 3u; ++k)
-        if (b + k < len)
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[t] >> (8u * k)), ors,
-                                               (int)(o + 4u * t + k), 0, 0);
+      for (uint32_t q = 0; q < 4u; ++q)
+        if (b + q < len) out_arena[o + 4u * t + q] = (uint8_t)(v[t] >> (8u * q));
     }
   }
 }
 
-__device__ __forceinline__ void store16_bytes(uint8_t *p, uint32_t lim, u32x4 v) {
-  for (uint32_t b = 0; b < 16u && b < lim; ++b) p[b] = (uint8_t)(v[b >> 2] >> (8u * (b & 3u)));
-}
-
-// ---- K5: rewrite + commit ----------------------------------------------------
+// ---- K5: rewrite (16 lanes per frame) + commit --------------------------------
 __global__ __launch_bounds__(kBlock) void nat64_rewrite(Nat64Args a) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= a.n) return;
-  const uint32_t ps = a.pkt_slot[i];
-  if (ps == kNoSlot) {
-    a.out_len[i] = 0;
+  const uint32_t g = threadIdx.x & (kGroup - 1u);
+  const uint32_t p = blockIdx.x * (kBlock / kGroup) + threadIdx.x / kGroup;
+  const bool valid = p < a.n;
+  const uint32_t ps = valid ? a.pkt_slot[p] : kNoSlot;
+  const uint32_t in_off = valid ? a.off[p] : 0u;
+  const uint32_t o_off = valid ? a.out_off[p] : 0u;
+  const bool in_al_wave = !__ballot((in_off & 3u) != 0u);
+  if (ps == kNoSlot) {  // uniform within the 16-lane group
+    if (valid && g == 0) a.out_len[p] = 0;
     return;
   }
-  const uint32_t slot = ps & ~kFirstBit;
+  const u32x4 hv = a.rec_h[p];
+  const uint2 bv = a.rec_b[p];
+  const uint32_t H[5] = {hv[0], hv[1], hv[2], hv[3], bv.x};
+  const uint32_t info = bv.y;
+  const uint32_t k = (info >> 8) & 3u, new_len = info >> 16;
+  const uint32_t port_be = swap16(a.pm.slot_port[ps & ~kFirstBit]);
+  const uint32_t span_lo = 34u + 4u * k;  // TCP header in the output frame
   const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
-  const uint32_t off = a.off[i];
-  const uint32_t len = a.len[i];
-  V6 v;
-  uint32_t P[24];
-  classify<24>(rs, a.arena_len, off, len, v, P);
-  const uint32_t k = v.k, eth_len = v.eth_len;
-  const uint32_t new_len = len - 20u;
-  const uint32_t port = a.pm.slot_port[slot];
-
-  // v6 fields (ip/v6/mod.rs:123-134, 172-200) and the pushed IPv4 header.
-  const uint32_t w = be32(v.L[0]);
-  const uint32_t dscp = (w & 0x0fc00000u) >> 22, ecn = (w & 0x00300000u) >> 20;
-  const uint32_t ttl = ((v.L[1] >> 24) - 1u) & 0xffu;  // hop_limit - 1 (u8, wrapping)
-  const uint32_t dscp_ecn = (((dscp << 2) & 0xfcu) | (ecn & 0x3u)) & 0xffu;
-  const uint32_t total_len = new_len - eth_len;
-  uint32_t H[5];
-  H[0] = 0x45u | (dscp_ecn << 8) | (swap16(total_len & 0xffffu) << 16);
-  H[1] = 0u;                   // identification 0, flags/frag 0 (v4.rs:594-609)
-  H[2] = ttl | (6u << 8);      // protocol = next_header (6); checksum below
-  H[3] = kV4Addr;              // V4_ADDR (main.rs:35)
-  H[4] = v.L[9];               // map6to4(dst): low 32 bits (main.rs:79-83)
-  const uint32_t ip_c =
-      (~swap16(fold64((uint64_t)H[0] + H[1] + H[2] + H[3] + H[4]))) & 0xffffu;
-  H[2] |= swap16(ip_c) << 16;
-  const uint32_t port_be = swap16(port);
-
-  const bool aligned = (a.out_off[i] & 3u) == 0u;
-  const uint32_t out_base = a.out_off[i];
   const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
-  uint8_t *obytes = a.out_arena + out_base;
+  const bool out_al = (o_off & 3u) == 0u;
 
-  // TCP span in output packet-relative bytes: [eth_len + 20, new_len).
-  const uint32_t span_dw = 8u + k;  // dword holding the span start (hi half)
-  uint64_t acc = 0;
-  u32x4 chunk3;
+  uint32_t acc = 0;
+  u32x4 held = {0u, 0u, 0u, 0u};  // chunk 3 holds the TCP checksum field (bytes 50+4k)
+  for (uint32_t q = 0; 256u * q < new_len; ++q) {
+    const uint32_t c = 16u * q + g;
+    if (16u * c >= new_len) continue;
+    // output byte b >= 34+4k comes from input byte b + 20 (the v6 header was
+    // 40 B, the v4 one is 20 B); bytes below 12+4k are the Ethernet header.
+    u32x4 o = load_in(rs, a.arena_len, in_off + 16u * c + 20u, in_al_wave);
+    if (c < 4u) {
+      const u32x4 A = load_in(rs, a.arena_len, in_off + 16u * c, in_al_wave);
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    u32x4 o;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int j = 4 * c + t;
-      const uint32_t d = out_dw(k, j, P, H, port_be);
-      o[t] = d;
-      uint32_t m = (uint32_t)j < span_dw ? 0u : end_mask(j, new_len);
-      if ((uint32_t)j == span_dw) m &= 0xffff0000u;
-      acc += (uint64_t)(d & m);
+      for (int t = 0; t < 4; ++t) {
+        const int r = (int)(4u * c) + t - (int)k;  // dword index relative to the VLAN depth
+        uint32_t d = o[t];
+        if (r < 3) d = A[t];                                       // Ethernet header
+        else if (r == 3) d = __builtin_amdgcn_alignbyte(H[0], 0x00080000u, 2);  // ether_type 0x0800
+        else if (r == 4) d = __builtin_amdgcn_alignbyte(H[1], H[0], 2);
+        else if (r == 5) d = __builtin_amdgcn_alignbyte(H[2], H[1], 2);
+        else if (r == 6) d = __builtin_amdgcn_alignbyte(H[3], H[2], 2);
+        else if (r == 7) d = __builtin_amdgcn_alignbyte(H[4], H[3], 2);
+        else if (r == 8) d = (H[4] >> 16) | (port_be << 16);  // dst tail | new TCP src port
+        else if (r == 12) d &= 0x0000ffffu;                     // TCP checksum zeroed
+        o[t] = d;
+      }
     }
-    if (c < 3) {
-      if (aligned) store16(ors, out_base, c, o, new_len);
-      else store16_bytes(obytes + 16 * c, new_len - 16u * c, o);
+    // this lane's share of the TCP span [34+4k, new_len)
+    if (16u * c >= span_lo && 16u * c + 16u <= new_len) {
+      acc = sad16(o[0], acc);
+      acc = sad16(o[1], acc);
+      acc = sad16(o[2], acc);
+      acc = sad16(o[3], acc);
     } else {
-      chunk3 = o;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc = sad16(o[t] & range_mask(16u * c + 4u * t, span_lo, new_len), acc);
     }
+    if (c == 3u) held = o;
+    else store_out(ors, a.out_arena, o_off, c, o, new_len, out_al);
   }
-  // Stream the rest: out dword j = input packet-relative dword j + 5.
-  const uint32_t sh = off & 3u, in_base = off - sh;
-  for (uint32_t c = 4; 16u * c < new_len; ++c) {
-    // input packet-relative dwords 4c+5 .. 4c+8 need absolute dwords 4c+5 .. 4c+9
-    const u32x4 q1 = load16(rs, in_base + 16u * (c + 1u), a.arena_len);
-    const u32x4 q2 = load16(rs, in_base + 16u * (c + 2u), a.arena_len);
-    u32x4 o;
-    o[0] = __builtin_amdgcn_alignbyte(q1[2], q1[1], sh);
-    o[1] = __builtin_amdgcn_alignbyte(q1[3], q1[2], sh);
-    o[2] = __builtin_amdgcn_alignbyte(q2[0], q1[3], sh);
-    o[3] = __builtin_amdgcn_alignbyte(q2[1], q2[0], sh);
+  // row reduction of the span sum (16 lanes = one DPP row)
+  acc += __shfl_xor(acc, 8, kGroup);
+  acc += __shfl_xor(acc, 4, kGroup);
+  acc += __shfl_xor(acc, 2, kGroup);
+  acc += __shfl_xor(acc, 1, kGroup);
+  if (g == 3u) {
+    // TCP checksum with the v4 pseudo-header (checksum.rs:93-103): src
+    // 203.0.113.1, dst, protocol 6, span length
+    const uint32_t span = (new_len - span_lo) & 0xffffu;
+    const uint32_t dst = be32(H[4]);
+    const uint32_t ph = fold32(0xcb00u + 0x7101u + (dst >> 16) + (dst & 0xffffu) + 6u + span);
+    const uint32_t tcp_c = (~fold32(ph + swap16(fold32(acc)))) & 0xffffu;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc += (uint64_t)(o[t] & end_mask((int)(4u * c) + t, new_len));
-    if (aligned) store16(ors, out_base, c, o, new_len);
-    else store16_bytes(obytes + 16u * c, new_len - 16u * c, o);
+    for (int t = 0; t < 4; ++t)
+      if ((uint32_t)t == k) held[t] |= swap16(tcp_c) << 16;
+    store_out(ors, a.out_arena, o_off, 3u, held, new_len, out_al);
   }
-  // TCP checksum with the v4 pseudo-header (checksum.rs:93-103).
-  const uint32_t span = (new_len - eth_len - 20u) & 0xffffu;
-  const uint32_t dst = be32(H[4]);
-  const uint32_t ph =
-      fold32(0xcb00u + 0x7101u + (dst >> 16) + (dst & 0xffffu) + 6u + span);  // 203.0.113.1
-  const uint32_t tcp_c = (~fold32(ph + swap16(fold64(acc)))) & 0xffffu;
-  // the checksum sits in the high half of output dword 12 + k (chunk 3)
-  const uint32_t cs_t = (12u + k) & 3u;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-    if ((uint32_t)t == cs_t) chunk3[t] |= swap16(tcp_c) << 16;
-  if (aligned) store16(ors, out_base, 3, chunk3, new_len);
-  else store16_bytes(obytes + 48, new_len - 48u, chunk3);
-
-  a.out_len[i] = (uint16_t)new_len;
-  if (ps & kFirstBit) {  // commit the new key (PORT_MAP.insert_new, main.rs:49)
-    uint32_t key[5];
-    make_key(v, key);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a.pm.key_src[4u * slot + j] = key[j];
-    a.pm.key_port[slot] = key[4];
-    a.pm.slot_min[slot] = 0xffffffffu;
-    a.pm.slot_ref[slot] = kPersist;
+  if (g == 0u) {
+    a.out_len[p] = (uint16_t)new_len;
+    if (ps & kFirstBit) {  // commit the new key (PORT_MAP.insert_new, main.rs:49)
+      const uint32_t slot = ps & ~kFirstBit;
+      a.pm.slot_min[slot] = 0xffffffffu;
+      a.pm.slot_ref[slot] = kPersist;
+    }
   }
 }
 
@@ -428,11 +464,12 @@ hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStr
 hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const uint32_t nb = nat64_num_blocks(a.n);
+  const uint32_t nb5 = (a.n + kBlock / kGroup - 1) / (kBlock / kGroup);
   hipLaunchKernelGGL(nat64_probe, dim3(nb), dim3(kBlock), 0, s, a);
   hipLaunchKernelGGL(nat64_count, dim3(nb), dim3(kBlock), 0, s, a);
   hipLaunchKernelGGL(nat64_scan, dim3(1), dim3(kScanBlock), 0, s, a, nb);
   hipLaunchKernelGGL(nat64_assign, dim3(nb), dim3(kBlock), 0, s, a);
-  hipLaunchKernelGGL(nat64_rewrite, dim3(nb), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(nat64_rewrite, dim3(nb5), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 

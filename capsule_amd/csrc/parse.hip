@@ -79,10 +79,12 @@ __device__ __forceinline__ uint32_t sum_to_end(const uint32_t (&Q)[kWin - 2], ui
 template <bool IPC, bool L4C, bool HASH, bool FIELDS>
 __global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= a.n) return;
+  // No early exit: lanes past n run with len 0 (status BadOffset) and store
+  // nothing, so the wave stays whole for the cooperative tail sum below.
+  const bool valid = i < a.n;
   const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
-  const uint32_t off = a.off[i];
-  const uint32_t len = a.len[i];
+  const uint32_t off = valid ? a.off[i] : 0u;
+  const uint32_t len = valid ? (uint32_t)a.len[i] : 0u;
 
   // --- the packet-relative window P ---------------------------------------
   uint32_t P[kWin];
@@ -193,11 +195,13 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
     ip_c = (~swap16(fold32(s))) & 0xffffu;
     if (ip_c == swap16(Q[6] & 0xffffu)) meta |= CGPU_META_IP_CSUM_OK;
   }
+  uint32_t s = 0, stored_le = 0;
+  bool has_tail = false;
   if (L4C && l4_ok) {
     // pseudo-header addresses + span [l4, len) (udp.rs:204-219, tcp.rs:
     // 462-477, checksum.rs:56-128) are one contiguous byte range: [26, len)
     // for v4, [22, len) for v6; the stored checksum field is subtracted.
-    uint32_t s = sad16(v6 ? (Q[5] & 0xffff0000u) : 0u, 0u);
+    s = sad16(v6 ? (Q[5] & 0xffff0000u) : 0u, 0u);
     s = sad16(v6 ? Q[6] : (Q[6] & 0xffff0000u), s);
     const uint32_t endn = len - 4u * k;  // normalized end of frame
     const uint32_t wend = endn < kQEnd ? endn : kQEnd;
@@ -206,21 +210,56 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
     } else {
       s = sum_to_end<7>(Q, wend, s);
     }
-    const uint32_t stored_le = udp ? (v6 ? (Q[15] & 0xffffu) : (Q[10] & 0xffffu))
-                                   : (v6 ? (Q[17] >> 16) : (Q[12] >> 16));
+    stored_le = udp ? (v6 ? (Q[15] & 0xffffu) : (Q[10] & 0xffffu))
+                    : (v6 ? (Q[17] >> 16) : (Q[12] >> 16));
     s -= stored_le;
-    if (endn > kQEnd) {  // span continues past the window: stream it
-      const uint32_t from = off + kQEnd + 4u * k;
-      uint32_t rt = fold64(sum_abs(rs, a.arena_len, from, off + len));
+    has_tail = endn > kQEnd;  // span continues past the window
+  }
+  if (L4C && __ballot(has_tail)) {
+    // The tails of the wave's long frames are summed by the whole wave, one
+    // frame at a time: 64 lanes x 16 B coalesced loads, v_sad_u16, a DPP
+    // reduction.  (Per-lane serial loops here were divergent AoS streams.)
+    const uint32_t t_from = off + kQEnd + 4u * k, t_to = off + len;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t tail = 0;
+    uint64_t m = __ballot(has_tail);
+    while (m) {
+      const int src_lane = __builtin_ctzll(m);
+      m &= m - 1;
+      const uint32_t from = __builtin_amdgcn_readlane(t_from, src_lane);
+      const uint32_t to = __builtin_amdgcn_readlane(t_to, src_lane);
+      uint32_t acc = 0;
+      for (uint32_t b = from & ~15u; b < to; b += 1024u) {
+        const uint32_t o = b + 16u * lane;
+        if (o < to) {
+          const u32x4 v = load16(rs, o, a.arena_len);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const uint32_t d = o + 4u * t;
+            uint32_t msk = 0xffffffffu;
+            if (d < from) msk = from - d >= 4u ? 0u : (0xffffffffu << (8u * (from - d)));
+            if (d + 4u > to) msk &= to <= d ? 0u : (0xffffffffu >> (8u * (d + 4u - to)));
+            acc = sad16(v[t] & msk, acc);
+          }
+        }
+      }
+      acc = __reduce_add_sync(~0ull, acc);
+      if (lane == (uint32_t)src_lane) tail = acc;
+    }
+    if (has_tail) {
+      uint32_t rt = fold32(tail);
       if (off & 1u) rt = swap16(rt);  // absolute parity -> packet parity
       s += rt;
     }
+  }
+  if (L4C && l4_ok) {
     const uint32_t span = (len - l4_off) & 0xffffu;
     l4_c = (~fold32(swap16(fold32(s)) + span + (udp ? 17u : 6u))) & 0xffffu;
     if (udp && l4_c == 0u) l4_c = 0xffffu;  // udp.rs:137-140
     if (l4_c == swap16(stored_le)) meta |= CGPU_META_L4_CSUM_OK;
   }
 
+  if (!valid) return;
   a.meta[i] = meta;
   if ((IPC || L4C) && a.csum != nullptr) a.csum[i] = ip_c | (l4_c << 16);
 

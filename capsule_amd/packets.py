@@ -275,3 +275,45 @@ class Nat64Gateway:
             self.close()
         except Exception:
             pass
+
+
+class ParseLauncher:
+    """A `parse` call with every ctypes argument prebuilt: calling it costs one
+    foreign call (for launch-bound loops such as bench.py; the batch and
+    output tensors must stay alive and unchanged in size)."""
+
+    def __init__(self, ctx, batch, out, flags, stream=None):
+        self._keep = (batch, out)
+        self._fn = N.lib().cgpu_parse_batch
+        self._args = [ctx.handle, None, flags, None, _stream_handle(stream)]
+        self._cb = batch.cbatch()
+        self._po = N.ParseOut()
+        self._po.meta = out.meta.data_ptr()
+        self._po.csum = out.csum.data_ptr() if out.csum is not None else None
+        self._po.flow_hash = out.flow_hash.data_ptr()
+        self._po.fields = out.fields.data_ptr() if out.fields is not None else None
+        self._args[1] = ctypes.byref(self._cb)
+        self._args[3] = ctypes.byref(self._po)
+
+    def __call__(self):
+        rc = self._fn(*self._args)
+        if rc:
+            N.check(rc, "cgpu_parse_batch")
+
+
+class Nat64Launcher:
+    """A `Nat64Gateway.nat_6to4` call with prebuilt ctypes arguments."""
+
+    def __init__(self, gw, batch, out, stream=None):
+        out_arena, out_off, out_len, disp, status = out
+        self._keep = (gw, batch, out)
+        self._cb = batch.cbatch()
+        self._fn = N.lib().cgpu_nat64_6to4
+        self._args = [gw.ctx.handle, gw._h, ctypes.byref(self._cb), _ptr(out_arena),
+                      out_arena.numel(), _ptr(out_off), _ptr(out_len), _ptr(disp), _ptr(status),
+                      _stream_handle(stream)]
+
+    def __call__(self):
+        rc = self._fn(*self._args)
+        if rc:
+            N.check(rc, "cgpu_nat64_6to4")

@@ -1,0 +1,13 @@
+#!/bin/bash
+# bench + rocprofv3 (stats, FETCH_SIZE, WRITE_SIZE) for every config.
+# usage: bash scripts/all_configs.sh <tag> [configs...]
+TAG=${1:-r03}; shift
+CONFIGS=${*:-parse64 imix imix_csum nat64}
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for c in $CONFIGS; do
+  timeout -k 10 300 python bench.py --config $c --steps 300 --warmup 30 --cpu-seconds 5 > gpurun_out/bench_$c.log 2>&1
+  rc=$?; echo "bench $c rc=$rc"; tail -1 gpurun_out/bench_$c.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+  bash scripts/profile.sh ${TAG}_$c --config $c --steps 100 --warmup 10 || exit $?
+done
