@@ -130,7 +130,7 @@ static int check_batch(const cgpu_batch *b) {
   if (!b) return CGPU_EINVAL;
   if (b->n == 0) return 0;
   if (!b->arena || !b->off || !b->len) return CGPU_EINVAL;
-  if (b->arena_len >= (1ull << 32)) return CGPU_EINVAL;
+  if (b->arena_len > 0xffff0000ull) return CGPU_EINVAL;  // offsets above are "no read"
   return 0;
 }
 

@@ -20,11 +20,11 @@
 //   K2 count   : per-workgroup count of "first packet of a new key".
 //   K3 scan    : exclusive scan of the counts (one workgroup) + NEXT_PORT.
 //   K4 assign  : ballot/popcount prefix -> ordinal -> port = base + ordinal.
-//   K5 rewrite : sixteen lanes (one DPP row) per frame.  Lane g builds output
-//                bytes [16c, 16c + 16), c = 16q + g, from coalesced loads of
-//                the shifted input, sums its share of the TCP span with
-//                v_sad_u16, the row reduces it, and the lane holding the TCP
-//                checksum field stores last; then the key is committed.
+//   K5 rewrite : four lanes per frame, four 16-B output chunks per lane,
+//                loaded from the input shifted by 20 bytes (16 loads of a
+//                256-B frame in flight per group), TCP span summed with
+//                v_sad_u16 and reduced across the group; the lane holding
+//                the TCP checksum field stores it last; keys are committed.
 // Kernel boundaries are the only cross-workgroup hand-offs besides the
 // device-scope atomics on slot_ref / slot_min.
 #include "capsule_gpu.h"
@@ -36,7 +36,8 @@ namespace cgpu {
 namespace {
 
 constexpr uint32_t kBlock = 256;
-constexpr uint32_t kGroup = 16;  // lanes per frame in K5 (one DPP row)
+constexpr uint32_t kGroup = 4;   // lanes per frame in K5
+constexpr uint32_t kChunks = 4;  // 16-B output chunks per lane per pass (kChunks >= 4)
 constexpr uint32_t kNoSlot = 0xffffffffu;
 constexpr uint32_t kFirstBit = 0x80000000u;  // pkt_slot: first packet of a new key
 constexpr uint32_t kV4Addr = 0x017100cbu;    // 203.0.113.1 as LE dword of wire bytes
@@ -346,7 +347,60 @@ __device__ __forceinline__ void store_out(rsrc_t ors, uint8_t *out_arena, uint32
   }
 }
 
-// ---- K5: rewrite (16 lanes per frame) + commit --------------------------------
+// Output dwords 0..15 (chunks 0..3) of the rewritten frame for VLAN depth K
+// (compile-time, so every select folds away), from the input dwords A (same
+// position) and o (input shifted by 20 bytes).  Returns the u16-word sum of
+// the TCP span bytes [34 + 4K, new_len) inside these chunks.
+template <int K>
+__device__ __forceinline__ uint32_t build_header(u32x4 (&o)[kChunks], const u32x4 (&A)[4],
+                                                 const uint32_t (&H)[5], uint32_t port_be,
+                                                 uint32_t new_len) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int r = 4 * n + t - K;
+      uint32_t d = o[n][t];
+      if (r < 3) d = A[n][t];                                                 // Ethernet
+      else if (r == 3) d = __builtin_amdgcn_alignbyte(H[0], 0x00080000u, 2);  // ether_type
+      else if (r == 4) d = __builtin_amdgcn_alignbyte(H[1], H[0], 2);
+      else if (r == 5) d = __builtin_amdgcn_alignbyte(H[2], H[1], 2);
+      else if (r == 6) d = __builtin_amdgcn_alignbyte(H[3], H[2], 2);
+      else if (r == 7) d = __builtin_amdgcn_alignbyte(H[4], H[3], 2);
+      else if (r == 8) d = (H[4] >> 16) | (port_be << 16);  // dst tail | TCP src port
+      else if (r == 12) d &= 0x0000ffffu;                     // TCP checksum zeroed
+      o[n][t] = d;
+      if (r >= 8) {  // TCP span: from the high half of dword 8 + K
+        uint32_t m = r == 8 ? 0xffff0000u : 0xffffffffu;
+        m &= range_mask(16u * n + 4u * t, 0u, new_len);
+        acc = sad16(d & m, acc);
+      }
+    }
+  }
+  return acc;
+}
+
+__device__ __forceinline__ uint32_t build_header_dyn(u32x4 (&o)[kChunks], const u32x4 (&A)[4],
+                                                     const uint32_t (&H)[5], uint32_t port_be,
+                                                     uint32_t new_len, uint32_t k) {
+  u32x4 o0[kChunks], o1[kChunks], o2[kChunks];
+#pragma unroll
+  for (uint32_t n = 0; n < kChunks; ++n) o0[n] = o1[n] = o2[n] = o[n];
+  const uint32_t s0 = build_header<0>(o0, A, H, port_be, new_len);
+  const uint32_t s1 = build_header<1>(o1, A, H, port_be, new_len);
+  const uint32_t s2 = build_header<2>(o2, A, H, port_be, new_len);
+#pragma unroll
+  for (uint32_t n = 0; n < 4u; ++n) o[n] = k == 0u ? o0[n] : (k == 1u ? o1[n] : o2[n]);
+  return k == 0u ? s0 : (k == 1u ? s1 : s2);
+}
+
+// ---- K5: rewrite (kGroup lanes per frame, kChunks x 16 B per lane) + commit --
+// Lane g of a frame's group builds output chunks c = (q*kGroup + g)*kChunks + n
+// (16 B each) from coalesced loads of the input shifted by 20 bytes; lane 0
+// of pass 0 owns chunks 0..3, i.e. the Ethernet/IPv4 header and the TCP
+// header up to its checksum field (output bytes 50+4k, chunk 3), and stores
+// chunk 3 after the group has reduced the TCP span sum.
 __global__ __launch_bounds__(kBlock) void nat64_rewrite(Nat64Args a) {
   const uint32_t g = threadIdx.x & (kGroup - 1u);
   const uint32_t p = blockIdx.x * (kBlock / kGroup) + threadIdx.x / kGroup;
@@ -355,65 +409,72 @@ __global__ __launch_bounds__(kBlock) void nat64_rewrite(Nat64Args a) {
   const uint32_t in_off = valid ? a.off[p] : 0u;
   const uint32_t o_off = valid ? a.out_off[p] : 0u;
   const bool in_al_wave = !__ballot((in_off & 3u) != 0u);
-  if (ps == kNoSlot) {  // uniform within the 16-lane group
+  if (ps == kNoSlot) {  // uniform within the group
     if (valid && g == 0) a.out_len[p] = 0;
     return;
   }
   const u32x4 hv = a.rec_h[p];
   const uint2 bv = a.rec_b[p];
+  const uint32_t port_be = swap16(a.pm.slot_port[ps & ~kFirstBit]);
   const uint32_t H[5] = {hv[0], hv[1], hv[2], hv[3], bv.x};
   const uint32_t info = bv.y;
   const uint32_t k = (info >> 8) & 3u, new_len = info >> 16;
-  const uint32_t port_be = swap16(a.pm.slot_port[ps & ~kFirstBit]);
   const uint32_t span_lo = 34u + 4u * k;  // TCP header in the output frame
   const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
   const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
   const bool out_al = (o_off & 3u) == 0u;
 
   uint32_t acc = 0;
-  u32x4 held = {0u, 0u, 0u, 0u};  // chunk 3 holds the TCP checksum field (bytes 50+4k)
-  for (uint32_t q = 0; 256u * q < new_len; ++q) {
-    const uint32_t c = 16u * q + g;
-    if (16u * c >= new_len) continue;
-    // output byte b >= 34+4k comes from input byte b + 20 (the v6 header was
-    // 40 B, the v4 one is 20 B); bytes below 12+4k are the Ethernet header.
-    u32x4 o = load_in(rs, a.arena_len, in_off + 16u * c + 20u, in_al_wave);
-    if (c < 4u) {
-      const u32x4 A = load_in(rs, a.arena_len, in_off + 16u * c, in_al_wave);
+  u32x4 held = {0u, 0u, 0u, 0u};
+  const uint32_t kw = __builtin_amdgcn_readfirstlane(k);
+  const bool k_uniform = !__ballot(k != kw);
+  for (uint32_t q = 0; 16u * kChunks * kGroup * q < new_len; ++q) {
+    const uint32_t c0 = (q * kGroup + g) * kChunks;
+    u32x4 o[kChunks];
+    // output byte b >= 34+4k is input byte b + 20 (v6 header 40 B -> v4 20 B)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int r = (int)(4u * c) + t - (int)k;  // dword index relative to the VLAN depth
-        uint32_t d = o[t];
-        if (r < 3) d = A[t];                                       // Ethernet header
-        else if (r == 3) d = __builtin_amdgcn_alignbyte(H[0], 0x00080000u, 2);  // ether_type 0x0800
-        else if (r == 4) d = __builtin_amdgcn_alignbyte(H[1], H[0], 2);
-        else if (r == 5) d = __builtin_amdgcn_alignbyte(H[2], H[1], 2);
-        else if (r == 6) d = __builtin_amdgcn_alignbyte(H[3], H[2], 2);
-        else if (r == 7) d = __builtin_amdgcn_alignbyte(H[4], H[3], 2);
-        else if (r == 8) d = (H[4] >> 16) | (port_be << 16);  // dst tail | new TCP src port
-        else if (r == 12) d &= 0x0000ffffu;                     // TCP checksum zeroed
-        o[t] = d;
+    for (uint32_t n = 0; n < kChunks; ++n) {
+      const uint32_t c = c0 + n;
+      o[n] = u32x4{0u, 0u, 0u, 0u};
+      if (16u * c < new_len) o[n] = load_in(rs, a.arena_len, in_off + 16u * c + 20u, in_al_wave);
+    }
+    if (c0 == 0u) {  // header region, output bytes 0..63 (lane 0 of pass 0)
+      u32x4 A[4];
+#pragma unroll
+      for (uint32_t n = 0; n < 4u; ++n) A[n] = load_in(rs, a.arena_len, in_off + 16u * n, in_al_wave);
+      if (k_uniform && kw == 0u) acc = build_header<0>(o, A, H, port_be, new_len);
+      else if (k_uniform && kw == 1u) acc = build_header<1>(o, A, H, port_be, new_len);
+      else if (k_uniform) acc = build_header<2>(o, A, H, port_be, new_len);
+      else acc = build_header_dyn(o, A, H, port_be, new_len, k);
+      held = o[3];
+    } else {
+      // whole chunks, then the bytes past new_len of the last one subtracted
+#pragma unroll
+      for (uint32_t n = 0; n < kChunks; ++n)
+        if (16u * (c0 + n) < new_len) acc = sad16(o[n][3], sad16(o[n][2], sad16(o[n][1], sad16(o[n][0], acc))));
+      const uint32_t pc = (new_len - 1u) >> 4;  // chunk holding the last byte
+      if ((new_len & 15u) != 0u && pc >= c0 && pc < c0 + kChunks) {
+        u32x4 last = o[0];
+#pragma unroll
+        for (uint32_t n = 1; n < kChunks; ++n)
+          if (pc == c0 + n) last = o[n];
+#pragma unroll
+        for (uint32_t t = 0; t < 4u; ++t) {
+          const uint32_t x = last[t] & ~range_mask(16u * pc + 4u * t, 0u, new_len);
+          acc -= (x & 0xffffu) + (x >> 16);
+        }
       }
     }
-    // this lane's share of the TCP span [34+4k, new_len)
-    if (16u * c >= span_lo && 16u * c + 16u <= new_len) {
-      acc = sad16(o[0], acc);
-      acc = sad16(o[1], acc);
-      acc = sad16(o[2], acc);
-      acc = sad16(o[3], acc);
-    } else {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc = sad16(o[t] & range_mask(16u * c + 4u * t, span_lo, new_len), acc);
+    for (uint32_t n = 0; n < kChunks; ++n) {
+      const uint32_t c = c0 + n;
+      if (16u * c < new_len && c != 3u) store_out(ors, a.out_arena, o_off, c, o[n], new_len, out_al);
     }
-    if (c == 3u) held = o;
-    else store_out(ors, a.out_arena, o_off, c, o, new_len, out_al);
   }
-  // row reduction of the span sum (16 lanes = one DPP row)
-  acc += __shfl_xor(acc, 8, kGroup);
-  acc += __shfl_xor(acc, 4, kGroup);
-  acc += __shfl_xor(acc, 2, kGroup);
-  acc += __shfl_xor(acc, 1, kGroup);
-  if (g == 3u) {
+  // group reduction of the span sum
+#pragma unroll
+  for (uint32_t d = kGroup / 2; d > 0; d >>= 1) acc += __shfl_xor(acc, d, kGroup);
+  if (g == 0u) {
     // TCP checksum with the v4 pseudo-header (checksum.rs:93-103): src
     // 203.0.113.1, dst, protocol 6, span length
     const uint32_t span = (new_len - span_lo) & 0xffffu;
@@ -424,8 +485,6 @@ __global__ __launch_bounds__(kBlock) void nat64_rewrite(Nat64Args a) {
     for (int t = 0; t < 4; ++t)
       if ((uint32_t)t == k) held[t] |= swap16(tcp_c) << 16;
     store_out(ors, a.out_arena, o_off, 3u, held, new_len, out_al);
-  }
-  if (g == 0u) {
     a.out_len[p] = (uint16_t)new_len;
     if (ps & kFirstBit) {  // commit the new key (PORT_MAP.insert_new, main.rs:49)
       const uint32_t slot = ps & ~kFirstBit;

@@ -36,6 +36,7 @@ namespace {
 constexpr uint32_t kBlock = 256;
 constexpr int kWin = 24;        // packet-relative window dwords (96 B)
 constexpr uint32_t kQEnd = 88;  // normalized window bytes valid after a QinQ shift
+constexpr uint32_t kNoRead = 0xffffff00u;  // > any arena_len the ABI accepts
 
 __device__ __forceinline__ uint32_t sel3(uint32_t k, uint32_t a, uint32_t b, uint32_t c) {
   return k == 0u ? a : (k == 1u ? b : c);
@@ -76,8 +77,33 @@ __device__ __forceinline__ uint32_t sum_to_end(const uint32_t (&Q)[kWin - 2], ui
   return acc;
 }
 
+// Tail sums.  A 1 KiB piece [b, b + 1024) of a tail [from, to) (absolute
+// arena offsets, b = from & ~15 + 1024 j) is loaded by the whole wave, 16 B
+// per lane; a lane loads its chunk only if the chunk overlaps [from, to), and
+// sums all 16 bytes without masks.  The bytes of the first and last chunk that
+// lie outside [from, to) are subtracted afterwards from wave-uniform copies of
+// those two chunks (v_readlane + scalar arithmetic).
+__device__ __forceinline__ uint32_t sum4(u32x4 v, uint32_t acc) {
+  return sad16(v[3], sad16(v[2], sad16(v[1], sad16(v[0], acc))));
+}
+
+// u16-word sum of the bytes of chunk [c, c + 16) outside [from, to).
+__device__ __forceinline__ uint32_t chunk_excess(u32x4 v, uint32_t c, uint32_t from, uint32_t to) {
+  uint32_t e = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < 4u; ++t) {
+    const uint32_t d = c + 4u * t;
+    uint32_t keep = 0xffffffffu;
+    if (from > d) keep = from >= d + 4u ? 0u : (0xffffffffu << (8u * (from - d)));
+    if (to < d + 4u) keep &= to <= d ? 0u : (0xffffffffu >> (8u * (d + 4u - to)));
+    const uint32_t x = v[t] & ~keep;
+    e += (x & 0xffffu) + (x >> 16);
+  }
+  return e;
+}
+
 template <bool IPC, bool L4C, bool HASH, bool FIELDS>
-__global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
+__global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   // No early exit: lanes past n run with len 0 (status BadOffset) and store
   // nothing, so the wave stays whole for the cooperative tail sum below.
@@ -215,54 +241,8 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
     s -= stored_le;
     has_tail = endn > kQEnd;  // span continues past the window
   }
-  if (L4C && __ballot(has_tail)) {
-    // The tails of the wave's long frames are summed by the whole wave, one
-    // frame at a time: 64 lanes x 16 B coalesced loads, v_sad_u16, a DPP
-    // reduction.  (Per-lane serial loops here were divergent AoS streams.)
-    const uint32_t t_from = off + kQEnd + 4u * k, t_to = off + len;
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t tail = 0;
-    uint64_t m = __ballot(has_tail);
-    while (m) {
-      const int src_lane = __builtin_ctzll(m);
-      m &= m - 1;
-      const uint32_t from = __builtin_amdgcn_readlane(t_from, src_lane);
-      const uint32_t to = __builtin_amdgcn_readlane(t_to, src_lane);
-      uint32_t acc = 0;
-      for (uint32_t b = from & ~15u; b < to; b += 1024u) {
-        const uint32_t o = b + 16u * lane;
-        if (o < to) {
-          const u32x4 v = load16(rs, o, a.arena_len);
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const uint32_t d = o + 4u * t;
-            uint32_t msk = 0xffffffffu;
-            if (d < from) msk = from - d >= 4u ? 0u : (0xffffffffu << (8u * (from - d)));
-            if (d + 4u > to) msk &= to <= d ? 0u : (0xffffffffu >> (8u * (d + 4u - to)));
-            acc = sad16(v[t] & msk, acc);
-          }
-        }
-      }
-      acc = __reduce_add_sync(~0ull, acc);
-      if (lane == (uint32_t)src_lane) tail = acc;
-    }
-    if (has_tail) {
-      uint32_t rt = fold32(tail);
-      if (off & 1u) rt = swap16(rt);  // absolute parity -> packet parity
-      s += rt;
-    }
-  }
-  if (L4C && l4_ok) {
-    const uint32_t span = (len - l4_off) & 0xffffu;
-    l4_c = (~fold32(swap16(fold32(s)) + span + (udp ? 17u : 6u))) & 0xffffu;
-    if (udp && l4_c == 0u) l4_c = 0xffffu;  // udp.rs:137-140
-    if (l4_c == swap16(stored_le)) meta |= CGPU_META_L4_CSUM_OK;
-  }
-
-  if (!valid) return;
-  a.meta[i] = meta;
-  if ((IPC || L4C) && a.csum != nullptr) a.csum[i] = ip_c | (l4_c << 16);
-
+  // Hash and header record first: only the checksum state stays live across
+  // the cooperative tail loop below (register pressure).
   // addresses as LE dwords of their wire bytes
   uint32_t src[4], dst[4];
   if (HASH || FIELDS) {
@@ -282,10 +262,10 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
     if (l4_ok) {  // Udp::flow / Tcp::flow (udp.rs:151-159, tcp.rs:409-417)
       h = flow_hash(v6, src, dst, be16_lo(U[0]), be16_hi(U[0]), udp ? 17u : 6u);
     }
-    a.hash[i] = h;
+    if (valid) a.hash[i] = h;
   }
 
-  if (FIELDS) {
+  if (FIELDS && valid) {
     uint32_t R[24];
 #pragma unroll
     for (int j = 0; j < 24; ++j) R[j] = 0u;
@@ -339,6 +319,84 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(ParseArgs a) {
       out[q] = v;
     }
   }
+  if (L4C && __ballot(has_tail)) {
+    // The tails of the wave's long frames (bytes past the register window) are
+    // summed by 16-lane groups, four frames at a time: in round r group j takes
+    // the (4r + j)-th long frame of the wave.  Its lanes load 16-B chunks
+    // 256 B apart, four per step in flight, sum them without masks, subtract
+    // the bytes of the first and last chunk that lie outside the tail, and the
+    // row reduces; the owner lane picks its sum up with a bpermute.
+    const uint32_t t_from = off + kQEnd + 4u * k, t_to = off + len;
+    const uint32_t lane = threadIdx.x & 63u, grp = lane >> 4, l16 = lane & 15u;
+    const uint64_t mall = __ballot(has_tail);
+    const uint32_t my_rank =
+        __builtin_amdgcn_mbcnt_hi((uint32_t)(mall >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mall, 0u));
+    // every chunk any tail needs lies inside the arena: branch-free loads
+    const bool fast = !__ballot(has_tail && (uint64_t)((t_to + 15u) & ~15u) > (uint64_t)a.arena_len);
+    uint32_t tail = 0;
+    uint64_t m = mall;
+    for (uint32_t r = 0; m; ++r) {
+      uint32_t own[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        own[u] = 64u;
+        if (m) {
+          own[u] = (uint32_t)__builtin_ctzll(m);
+          m &= m - 1;
+        }
+      }
+      const uint32_t mine = grp == 0u ? own[0] : (grp == 1u ? own[1] : (grp == 2u ? own[2] : own[3]));
+      const bool active = mine < 64u;
+      const uint32_t src = active ? mine : 0u;
+      const uint32_t fr = __shfl(t_from, src), to = __shfl(t_to, src);
+      uint32_t acc = 0;
+      if (active) {
+        const uint32_t b = fr & ~15u, ct = (to - 1u) & ~15u;
+        for (uint32_t base = b; base < to; base += 1024u) {
+          u32x4 v[4];
+#pragma unroll
+          for (uint32_t it = 0; it < 4u; ++it) {
+            const uint32_t o = base + 256u * it + 16u * l16;
+            const bool need = o < to;
+            if (fast) {
+              v[it] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(need ? o : kNoRead), 0, 0);
+            } else {
+              v[it] = u32x4{0u, 0u, 0u, 0u};
+              if (need) v[it] = load16(rs, o, a.arena_len);
+            }
+          }
+#pragma unroll
+          for (uint32_t it = 0; it < 4u; ++it) acc = sum4(v[it], acc);
+#pragma unroll
+          for (uint32_t it = 0; it < 4u; ++it) {
+            const uint32_t o = base + 256u * it + 16u * l16;
+            if (o == b || o == ct) acc -= chunk_excess(v[it], o, fr, to);
+          }
+        }
+      }
+#pragma unroll
+      for (uint32_t d = 8; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 16);
+      const bool mine_now = has_tail && my_rank >= 4u * r && my_rank < 4u * r + 4u;
+      const uint32_t got = __shfl(acc, mine_now ? (my_rank - 4u * r) * 16u : 0u);
+      if (mine_now) tail = got;
+    }
+    if (has_tail) {
+      uint32_t rt = fold32(tail);
+      if (off & 1u) rt = swap16(rt);  // absolute parity -> packet parity
+      s += rt;
+    }
+  }
+  if (L4C && l4_ok) {
+    const uint32_t span = (len - l4_off) & 0xffffu;
+    l4_c = (~fold32(swap16(fold32(s)) + span + (udp ? 17u : 6u))) & 0xffffu;
+    if (udp && l4_c == 0u) l4_c = 0xffffu;  // udp.rs:137-140
+    if (l4_c == swap16(stored_le)) meta |= CGPU_META_L4_CSUM_OK;
+  }
+
+  if (!valid) return;
+  a.meta[i] = meta;
+  if ((IPC || L4C) && a.csum != nullptr) a.csum[i] = ip_c | (l4_c << 16);
+
 }
 
 template <bool IPC, bool L4C, bool HASH, bool FIELDS>

@@ -102,7 +102,7 @@ enum cgpu_pkt_status {
  * A batch is an arena of packet bytes plus one (offset, data_len) pair per
  * packet: the device image of a burst of single-segment mbufs
  * (buf_addr + data_off, data_len; mbuf.rs:196-205).  All pointers are
- * device pointers for the *_batch entry points.  arena_len must be < 2^32.  */
+ * device pointers for the *_batch entry points.  arena_len must be <= 0xFFFF0000.    */
 typedef struct cgpu_batch {
   const uint8_t *arena;
   uint64_t arena_len;
