@@ -152,6 +152,8 @@ def main():
                     choices=["parse64", "imix", "imix_csum", "nat64"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--e2e", action="store_true",
+                    help="host-resident batches: pinned H2D + parse + D2H, pipelined (DESIGN.md §8)")
     args = ap.parse_args()
 
     import torch
@@ -160,6 +162,8 @@ def main():
     from capsule_amd import packets
     from capsule_amd.shards import ShardGroup
 
+    if args.e2e:
+        return e2e(args)
     g = ShardGroup()
     dev = torch.device("cuda", g.local_rank)
     torch.cuda.set_device(dev)
@@ -260,6 +264,98 @@ def main():
         print(json.dumps(result), flush=True)
     ctx.close()
     g.close()
+
+
+def e2e(args):
+    """End-to-end rate with the batch starting and ending in host memory.
+
+    The burst sits in a pinned host arena (where a NIC would have DMA'd it);
+    each step copies arena + descriptors host->device on one stream, parses on
+    a second, copies meta/hash (and the nat64 output frames) device->host on a
+    third, with three batches in flight.  Prints one JSON line (not the
+    driver's metric line).
+    """
+    import torch
+
+    from capsule_amd import packets
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    w = make_workload(args.config, 0xC0FFEE + 2)
+    n = len(w["off"])
+    ctx = packets.Context(0)
+    host = dict(arena=torch.from_numpy(w["arena"]).pin_memory(),
+                off=torch.from_numpy(w["off"].view(np.int32)).pin_memory(),
+                len=torch.from_numpy(w["len"].view(np.int16)).pin_memory())
+    D = 3
+    bufs = [packets.PacketBatch(torch.empty_like(host["arena"], device=dev),
+                                torch.empty_like(host["off"], device=dev),
+                                torch.empty_like(host["len"], device=dev)) for _ in range(D)]
+    h2d, comp, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    if w["kind"] == "parse":
+        outs = [packets.ParseBuffers(n, dev, csum=False) for _ in range(D)]
+        host_out = [(torch.empty(n, dtype=torch.int32, pin_memory=True),
+                     torch.empty(n, dtype=torch.int64, pin_memory=True)) for _ in range(D)]
+        launch = [packets.ParseLauncher(ctx, bufs[d], outs[d], w["flags"], comp) for d in range(D)]
+
+        def back(d):
+            host_out[d][0].copy_(outs[d].meta, non_blocking=True)
+            host_out[d][1].copy_(outs[d].flow_hash, non_blocking=True)
+        down_bytes = 12 * n
+    else:
+        gw = packets.Nat64Gateway(ctx, capacity_log2=17)
+        nat = [(torch.empty_like(bufs[d].arena), bufs[d].off,
+                torch.empty(n, dtype=torch.int16, device=dev),
+                torch.empty(n, dtype=torch.uint8, device=dev),
+                torch.empty(n, dtype=torch.uint8, device=dev)) for d in range(D)]
+        host_out = [(torch.empty_like(host["arena"], pin_memory=True),
+                     torch.empty(n, dtype=torch.int16, pin_memory=True)) for _ in range(D)]
+        launch = [packets.Nat64Launcher(gw, bufs[d], nat[d], comp) for d in range(D)]
+
+        def back(d):
+            host_out[d][0].copy_(nat[d][0], non_blocking=True)
+            host_out[d][1].copy_(nat[d][2], non_blocking=True)
+        down_bytes = len(w["arena"]) + 2 * n
+    up_bytes = len(w["arena"]) + 6 * n
+    ev_up = [torch.cuda.Event() for _ in range(D)]
+    ev_comp = [torch.cuda.Event() for _ in range(D)]
+    ev_down = [torch.cuda.Event() for _ in range(D)]
+
+    def step(k):
+        d = k % D
+        with torch.cuda.stream(h2d):
+            h2d.wait_event(ev_down[d])  # buffer d free again (its results went home)
+            bufs[d].arena.copy_(host["arena"], non_blocking=True)
+            bufs[d].off.copy_(host["off"], non_blocking=True)
+            bufs[d].len.copy_(host["len"], non_blocking=True)
+            ev_up[d].record(h2d)
+        comp.wait_event(ev_up[d])
+        launch[d]()
+        ev_comp[d].record(comp)
+        with torch.cuda.stream(d2h):
+            d2h.wait_event(ev_comp[d])
+            back(d)
+            ev_down[d].record(d2h)
+
+    for d in range(D):
+        ev_down[d].record(d2h)
+    for k in range(max(3, args.warmup // 10)):
+        step(k)
+    torch.cuda.synchronize(dev)
+    steps = max(10, args.steps // 10)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": "end-to-end Mpps, host-resident batches (pinned H2D + kernel + D2H)",
+        "value": round(n * steps / el / 1e6, 2), "unit": "Mpps", "config": args.config,
+        "steps": steps, "packets_per_step": n, "ms_per_step": round(el / steps * 1e3, 3),
+        "h2d_GBps": round(up_bytes * steps / el / 1e9, 2),
+        "d2h_GBps": round(down_bytes * steps / el / 1e9, 2),
+        "batches_in_flight": D}), flush=True)
+    ctx.close()
 
 
 if __name__ == "__main__":

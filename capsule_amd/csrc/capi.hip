@@ -243,11 +243,11 @@ int cgpu_parse_host(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *le
 
 int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_port,
                         cgpu_portmap **out) {
-  if (!ctx || !out || capacity_log2 < 4 || capacity_log2 > 30) return fail(CGPU_EINVAL);
+  if (!ctx || !out || capacity_log2 < 4 || capacity_log2 > 29) return fail(CGPU_EINVAL);
   *out = nullptr;
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
   const size_t cap = (size_t)1 << capacity_log2;
-  const size_t bytes = cap * 4 * (1 + 1 + 4 + 1 + 1) + 256;
+  const size_t bytes = 256 + 65536 * 8 + cap * sizeof(cgpu::PortSlot);
   void *mem = nullptr;
   if (hipMalloc(&mem, bytes) != hipSuccess) return fail(CGPU_ENOMEM);
   cgpu_portmap *pm = new (std::nothrow) cgpu_portmap();
@@ -257,18 +257,10 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
   }
   pm->ctx = ctx;
   pm->mem = mem;
-  uint32_t *p = (uint32_t *)mem;
-  pm->dev.state = p;
-  p += 64;
-  pm->dev.slot_ref = p;
-  p += cap;
-  pm->dev.slot_min = p;
-  p += cap;
-  pm->dev.key_src = p;
-  p += 4 * cap;
-  pm->dev.key_port = p;
-  p += cap;
-  pm->dev.slot_port = p;
+  uint8_t *p = (uint8_t *)mem;
+  pm->dev.state = (uint32_t *)p;
+  pm->dev.rev = (uint64_t *)(p + 256);
+  pm->dev.slots = (cgpu::PortSlot *)(p + 256 + 65536 * 8);
   pm->dev.cap_mask = (uint32_t)(cap - 1);
   if (cgpu::launch_portmap_init(pm->dev, first_port, ctx->stream) != hipSuccess ||
       hipStreamSynchronize(ctx->stream) != hipSuccess) {
@@ -312,14 +304,14 @@ int cgpu_portmap_size(cgpu_portmap *pm, uint32_t *entries) {
   return ok();
 }
 
-int cgpu_nat64_6to4(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8_t *out_arena,
+static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8_t *out_arena,
                     uint64_t out_arena_len, const uint32_t *out_off, uint16_t *out_len,
                     uint8_t *disposition, uint8_t *status, void *stream) {
   if (!ctx || !pm) return fail(CGPU_EINVAL);
   if (int e = check_batch(in)) return fail(e);
   if (in->n == 0) return ok();
   if (!out_arena || !out_off || !out_len || !disposition || !status) return fail(CGPU_EINVAL);
-  if (out_arena_len >= (1ull << 32)) return fail(CGPU_EINVAL);
+  if (out_arena_len > 0xffff0000ull) return fail(CGPU_EINVAL);
   if (in->n >= 0x7fffffffu) return fail(CGPU_EINVAL);
   if (pm->scratch_n < in->n) {
     if (pm->pkt_slot) (void)hipFree(pm->pkt_slot);
@@ -329,7 +321,7 @@ int cgpu_nat64_6to4(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8
     void *m = nullptr;
     const size_t o_sums = align_up(4ull * in->n, 256);
     const size_t o_rech = o_sums + align_up(4ull * nb, 256);
-    const size_t o_recb = o_rech + align_up(16ull * in->n, 256);
+    const size_t o_recb = o_rech + align_up(48ull * in->n, 256);
     if (hipMalloc(&m, o_recb + 8ull * in->n + 256) != hipSuccess) return fail(CGPU_ENOMEM);
     pm->pkt_slot = (uint32_t *)m;
     pm->block_sums = (uint32_t *)((uint8_t *)m + o_sums);
@@ -354,9 +346,24 @@ int cgpu_nat64_6to4(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8
   a.rec_h = (cgpu::u32x4 *)pm->rec_h;
   a.rec_b = (uint2 *)pm->rec_b;
   a.pm = pm->dev;
-  hipError_t e = cgpu::launch_nat64_6to4(a, (hipStream_t)stream);
+  hipError_t e = to4 ? cgpu::launch_nat64_6to4(a, (hipStream_t)stream)
+                     : cgpu::launch_nat64_4to6(a, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e);
   return ok();
+}
+
+int cgpu_nat64_6to4(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8_t *out_arena,
+                    uint64_t out_arena_len, const uint32_t *out_off, uint16_t *out_len,
+                    uint8_t *disposition, uint8_t *status, void *stream) {
+  return nat64_call(true, ctx, pm, in, out_arena, out_arena_len, out_off, out_len, disposition,
+                    status, stream);
+}
+
+int cgpu_nat64_4to6(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8_t *out_arena,
+                    uint64_t out_arena_len, const uint32_t *out_off, uint16_t *out_len,
+                    uint8_t *disposition, uint8_t *status, void *stream) {
+  return nat64_call(false, ctx, pm, in, out_arena, out_arena_len, out_off, out_len, disposition,
+                    status, stream);
 }
 
 }  // extern "C"

@@ -28,18 +28,26 @@ hipError_t launch_parse(const ParseArgs &a, uint32_t flags, hipStream_t s);
 
 // ---- nat64 6to4 ------------------------------------------------------------
 // Device port map (examples/nat64/main.rs:37-53): open addressing, linear
-// probing.  slot_ref: 0 empty, kPersist = committed entry whose key lives in
-// key_src/key_port, else (packet index + 1) of a representative packet of
-// the batch in flight.
+// probing over 32-byte slots (PortSlot).  A slot's ref word is 0 (empty),
+// kPersist (committed; its key words are valid) or (packet index + 1) of a
+// representative packet of the batch in flight.
 constexpr uint32_t kPersist = 0x80000000u;
 
+// One slot of the device port map, 32 bytes (two dwordx4, one cache line
+// half): a lookup is a single line.
+//   w[0] ref   0 empty | kPersist committed | (packet index + 1) batch-local
+//   w[1..4]    key: v6 source address (wire bytes as LE dwords)
+//   w[5]       key: v6-side TCP source port
+//   w[6]       assigned gateway port
+//   w[7]       min packet index of the current batch (0xffffffff idle)
+struct PortSlot {
+  uint32_t w[8];
+};
+
 struct PortMapDev {
-  uint32_t *slot_ref;   // [cap]
-  uint32_t *slot_min;   // [cap] min packet index of the batch (0xffffffff idle)
-  uint32_t *key_src;    // [cap * 4] v6 source address, wire bytes as LE dwords
-  uint32_t *key_port;   // [cap] v6-side TCP source port
-  uint32_t *slot_port;  // [cap] assigned gateway port
-  uint32_t *state;      // [4]: next_port, entries, batch_base, batch_new
+  PortSlot *slots;  // [cap]
+  uint64_t *rev;    // [65536]: (first ordinal << 32 | slot), ~0 = none (ADDR_MAP, main.rs:38)
+  uint32_t *state;  // [4]: next_port, entries, batch_base, batch_new
   uint32_t cap_mask;
 };
 
@@ -57,12 +65,14 @@ struct Nat64Args {
   uint8_t *status;
   uint32_t *pkt_slot;    // scratch [n]: table slot (or 0xffffffff)
   uint32_t *block_sums;  // scratch [nblocks + 1]
-  u32x4 *rec_h;          // scratch [n]: new IPv4 header dwords 0..3 (K1 -> K5)
+  u32x4 *rec_h;          // scratch [3n]: new IPv4 header dwords 0..3 (6to4) or the
+                         // IPv6 header + port + pseudo-header sum, 48 B (4to6)
   uint2 *rec_b;          // scratch [n]: header dword 4, eth_len | k << 8 | new_len << 16
   PortMapDev pm;
 };
 
 hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s);
+hipError_t launch_nat64_4to6(const Nat64Args &a, hipStream_t s);
 hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStream_t s);
 uint32_t nat64_num_blocks(uint32_t n);
 

@@ -239,18 +239,13 @@ class Nat64Gateway:
         N.check(N.lib().cgpu_portmap_size(self._h, ctypes.byref(v)), "size")
         return v.value
 
-    def nat_6to4(self, batch, out_arena=None, out_off=None, stream=None, out=None):
-        """Returns (out PacketBatch, disposition u8, status u8) on the device.
-
-        Output frame i is written at out_off[i] (default: in place of its
-        input slot in a fresh arena of the same size); out_len[i] is the new
-        data_len for ACT packets and 0 otherwise.
-        """
+    def _call(self, fn, what, grow, batch, out_arena, out_off, stream, out):
         n = batch.n
         dev = batch.arena.device
         if out is None:
             if out_arena is None:
-                out_arena = torch.zeros_like(batch.arena)
+                out_arena = torch.zeros(batch.arena.numel() + grow * n, dtype=torch.uint8,
+                                        device=dev)
             if out_off is None:
                 out_off = batch.off
             out_len = torch.zeros(n, dtype=torch.int16, device=dev)
@@ -259,11 +254,27 @@ class Nat64Gateway:
         else:
             out_arena, out_off, out_len, disp, status = out
         cb = batch.cbatch()
-        rc = N.lib().cgpu_nat64_6to4(
-            self.ctx.handle, self._h, ctypes.byref(cb), _ptr(out_arena), out_arena.numel(),
-            _ptr(out_off), _ptr(out_len), _ptr(disp), _ptr(status), _stream_handle(stream))
-        N.check(rc, "cgpu_nat64_6to4")
+        rc = fn(self.ctx.handle, self._h, ctypes.byref(cb), _ptr(out_arena), out_arena.numel(),
+                _ptr(out_off), _ptr(out_len), _ptr(disp), _ptr(status), _stream_handle(stream))
+        N.check(rc, what)
         return PacketBatch(out_arena, out_off, out_len), disp, status
+
+    def nat_6to4(self, batch, out_arena=None, out_off=None, stream=None, out=None):
+        """`nat_6to4` (examples/nat64/main.rs:121-150) on a device batch.
+
+        Returns (out PacketBatch, disposition u8, status u8).  Output frame i
+        is written at out_off[i] (default: its input slot offset in a fresh
+        arena of the same size); out_len[i] is the new data_len for ACT
+        packets and 0 otherwise.
+        """
+        return self._call(N.lib().cgpu_nat64_6to4, "cgpu_nat64_6to4", 0, batch, out_arena,
+                          out_off, stream, out)
+
+    def nat_4to6(self, batch, out_arena, out_off, stream=None, out=None):
+        """`nat_4to6` (examples/nat64/main.rs:86-118): output frames are 20 B
+        longer, so out_off[i] must leave room for len[i] + 20 bytes."""
+        return self._call(N.lib().cgpu_nat64_4to6, "cgpu_nat64_4to6", 20, batch, out_arena,
+                          out_off, stream, out)
 
     def close(self):
         if self._h:

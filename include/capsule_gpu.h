@@ -212,6 +212,18 @@ int cgpu_nat64_6to4(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in,
                     uint8_t *out_arena, uint64_t out_arena_len, const uint32_t *out_off,
                     uint16_t *out_len, uint8_t *disposition, uint8_t *status, void *stream);
 
+/* ---- examples/nat64 4to6 -------------------------------------------------
+ * IPv4 -> IPv6 rewrite of examples/nat64/main.rs:86-118: TCP frames that are
+ * not fragments and whose destination port the 6to4 direction assigned
+ * (ADDR_MAP, :38, :56-58 — the same cgpu_portmap) become IPv6 frames to the
+ * original v6 source and port, from 64:ff9b::<v4 src>; everything else is
+ * DROP (or ABORT on a parse error).  Output frames are 20 bytes longer than
+ * the input (out_off[i] must leave room for len[i] + 20 bytes).  Same
+ * argument conventions as cgpu_nat64_6to4.                                   */
+int cgpu_nat64_4to6(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in,
+                    uint8_t *out_arena, uint64_t out_arena_len, const uint32_t *out_off,
+                    uint16_t *out_len, uint8_t *disposition, uint8_t *status, void *stream);
+
 /* ---- errors -------------------------------------------------------------- */
 int cgpu_last_error(void);
 const char *cgpu_strerror(int code);

@@ -399,6 +399,9 @@ struct or_portmap {
   pm_slot *slots;
   uint32_t cap, size;
   uint16_t next_port; /* AtomicU16 NEXT_PORT (main.rs:42), initial 1025 */
+  /* ADDR_MAP (main.rs:38): gateway port -> (v6 addr, port), insert_new */
+  uint8_t addr_key[65536][18];
+  uint8_t addr_used[65536];
 };
 
 or_portmap *or_portmap_new(uint16_t first_port) {
@@ -457,6 +460,10 @@ static uint16_t assigned_port(or_portmap *pm, const uint8_t addr[16], uint16_t p
   s->port = p;
   s->used = 1;
   pm->size++;
+  if (!pm->addr_used[p]) { /* ADDR_MAP.insert_new(port, key): first one stays */
+    memcpy(pm->addr_key[p], k, 18);
+    pm->addr_used[p] = 1;
+  }
   if (pm->size * 2 > pm->cap) pm_grow(pm);
   return p;
 }
@@ -521,6 +528,96 @@ static int nat_6to4(or_portmap *pm, mbuf_t *m, uint8_t *status) {
   wr16(h4 + 10, 0);
   wr16(h4 + 10, or_compute(0, h4, 20));
   return CGPU_ACT;
+}
+
+/* main.rs:86-118 nat_4to6 on one mbuf; returns disposition, sets *status. */
+static int nat_4to6(or_portmap *pm, mbuf_t *m, uint8_t *status) {
+  uint8_t *p = mb_data(m, 0);
+  /* let ethernet = packet.parse::<Ethernet>()?; */
+  eth_t e;
+  int st = eth_parse(p, m->data_len, &e);
+  if (st) { *status = (uint8_t)st; return CGPU_ABORT; }
+  /* let v4 = ethernet.parse::<Ipv4>()?; */
+  if (e.ether_type != 0x0800) { *status = CGPU_PKT_NOT_IPV4; return CGPU_ABORT; }
+  const uint32_t v4_off = e.header_len;
+  st = read_data(m->data_len, v4_off, 20, CGPU_PKT_L3_BAD_OFFSET, CGPU_PKT_L3_OUT_OF_BUFFER);
+  if (st) { *status = (uint8_t)st; return CGPU_ABORT; }
+  const uint8_t *h4 = p + v4_off;
+  *status = CGPU_PKT_OK;
+  /* if protocol == Tcp && fragment_offset() == 0 && !more_fragments() */
+  const uint16_t ff = rd16(h4 + 6);
+  if (!(h4[9] == 6 && (ff & 0x1fff) == 0 && !(ff & 0x2000))) return CGPU_DROP;
+  /* let tcp = v4.peek::<Tcp4>()?; */
+  const uint32_t tcp_off = v4_off + 20;
+  st = read_data(m->data_len, tcp_off, 20, CGPU_PKT_L4_BAD_OFFSET, CGPU_PKT_L4_OUT_OF_BUFFER);
+  if (st) { *status = (uint8_t)st; return CGPU_ABORT; }
+  /* if let Some((dst, port)) = assigned_addr(tcp.dst_port()) (main.rs:56-58) */
+  const uint16_t gw_port = rd16(p + tcp_off + 2);
+  if (!pm->addr_used[gw_port]) return CGPU_DROP;
+  uint8_t dst6[16];
+  memcpy(dst6, pm->addr_key[gw_port], 16);
+  const uint16_t orig_port = rd16(pm->addr_key[gw_port] + 16);
+  const uint8_t dscp = h4[1] >> 2, ecn = h4[1] & 0x03; /* v4.rs:186-203 */
+  const uint8_t next_header = h4[9];
+  const uint8_t hop_limit = (uint8_t)(h4[8] - 1); /* ttl - 1 (wrapping, release build) */
+  /* map4to6(v4.src()) = 64:ff9b::a.b.c.d (main.rs:62-74) */
+  uint8_t src6[16] = {0x00, 0x64, 0xff, 0x9b, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  memcpy(src6 + 12, h4 + 12, 4);
+  /* let ethernet = v4.remove()?;  (shrink(offset, 20)) */
+  if (mb_shrink(m, v4_off, 20)) { *status = CGPU_PKT_NOT_RESIZED; return CGPU_ABORT; }
+  /* let mut v6 = ethernet.push::<Ipv6>()?;  (ip/v6/mod.rs:302-316) */
+  if (mb_extend(m, v4_off, 40)) { *status = CGPU_PKT_NOT_RESIZED; return CGPU_ABORT; }
+  p = mb_data(m, 0);
+  uint8_t *h6 = p + v4_off;
+  memset(h6, 0, 40); /* Ipv6Header::default (:453-464) */
+  h6[0] = 0x60;
+  h6[7] = 64;
+  wr16(p + e.et_off, 0x86DD); /* envelope.set_ether_type(Ipv6) */
+  /* setters (ip/v6/mod.rs:130-209) */
+  uint32_t w = rd32(h6);
+  w = (w & ~0x0fc00000u) | (((uint32_t)dscp << 22) & 0x0fc00000u);
+  w = (w & ~0x00300000u) | (((uint32_t)ecn << 20) & 0x00300000u);
+  h6[0] = (uint8_t)(w >> 24); h6[1] = (uint8_t)(w >> 16); h6[2] = (uint8_t)(w >> 8); h6[3] = (uint8_t)w;
+  h6[6] = next_header;
+  h6[7] = hop_limit;
+  memcpy(h6 + 8, src6, 16);
+  memcpy(h6 + 24, dst6, 16);
+  /* let mut tcp = v6.parse::<Tcp6>()?; */
+  const uint32_t tcp6_off = v4_off + 40;
+  if (h6[6] != 6) { *status = CGPU_PKT_NOT_TCP; return CGPU_ABORT; }
+  st = read_data(m->data_len, tcp6_off, 20, CGPU_PKT_L4_BAD_OFFSET, CGPU_PKT_L4_OUT_OF_BUFFER);
+  if (st) { *status = (uint8_t)st; return CGPU_ABORT; }
+  uint8_t *t = p + tcp6_off;
+  wr16(t + 2, orig_port); /* tcp.set_dst_port(port) */
+  /* tcp.reconcile_all(): Tcp::compute_checksum with the v6 pseudo-header */
+  const uint32_t span = m->data_len - tcp6_off;
+  wr16(t + 16, 0);
+  const uint16_t ph = or_pseudo_v6(h6 + 8, h6 + 24, (uint16_t)span, 6);
+  wr16(t + 16, or_compute(ph, t, span));
+  /* Ipv6::reconcile (ip/v6/mod.rs:331-334): payload_length */
+  wr16(h6 + 4, (uint16_t)(m->data_len - v4_off - 40));
+  return CGPU_ACT;
+}
+
+void or_nat64_4to6(or_portmap *pm, const uint8_t *arena, const uint32_t *off, const uint16_t *len,
+                   uint32_t n, uint8_t *out_arena, const uint32_t *out_off, uint16_t *out_len,
+                   uint8_t *disposition, uint8_t *status) {
+  mbuf_t *m = (mbuf_t *)malloc(sizeof(mbuf_t));
+  for (uint32_t i = 0; i < n; ++i) {
+    m->data_off = MBUF_HEADROOM;
+    m->data_len = len[i];
+    if (m->data_len > MBUF_BUF_LEN - MBUF_HEADROOM) m->data_len = MBUF_BUF_LEN - MBUF_HEADROOM;
+    memcpy(mb_data(m, 0), arena + off[i], m->data_len);
+    int d = nat_4to6(pm, m, status + i);
+    disposition[i] = (uint8_t)d;
+    if (d == CGPU_ACT) {
+      memcpy(out_arena + out_off[i], mb_data(m, 0), m->data_len);
+      out_len[i] = (uint16_t)m->data_len;
+    } else {
+      out_len[i] = 0;
+    }
+  }
+  free(m);
 }
 
 void or_nat64_6to4(or_portmap *pm, const uint8_t *arena, const uint32_t *off, const uint16_t *len,

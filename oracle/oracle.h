@@ -60,6 +60,11 @@ void or_nat64_6to4(or_portmap *pm, const uint8_t *arena, const uint32_t *off, co
                    uint32_t n, uint8_t *out_arena, const uint32_t *out_off, uint16_t *out_len,
                    uint8_t *disposition, uint8_t *status);
 
+/* examples/nat64 4to6 (main.rs:86-118) with the same port map's ADDR_MAP. */
+void or_nat64_4to6(or_portmap *pm, const uint8_t *arena, const uint32_t *off, const uint16_t *len,
+                   uint32_t n, uint8_t *out_arena, const uint32_t *out_off, uint16_t *out_len,
+                   uint8_t *disposition, uint8_t *status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,6 +50,8 @@ def load(name="liboracle.so"):
     L.or_portmap_size.argtypes = [vp]
     L.or_nat64_6to4.restype = None
     L.or_nat64_6to4.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
+    L.or_nat64_4to6.restype = None
+    L.or_nat64_4to6.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
     return L
 
 
@@ -93,6 +95,12 @@ class PortMap:
         return lib().or_portmap_size(self.h)
 
     def nat_6to4(self, arena, off, length, out_off=None, out_size=None):
+        return self._nat(lib().or_nat64_6to4, arena, off, length, out_off, out_size)
+
+    def nat_4to6(self, arena, off, length, out_off, out_size):
+        return self._nat(lib().or_nat64_4to6, arena, off, length, out_off, out_size)
+
+    def _nat(self, fn, arena, off, length, out_off, out_size):
         n = len(off)
         arena = np.ascontiguousarray(arena, np.uint8)
         off = np.ascontiguousarray(off, np.uint32)
@@ -102,8 +110,8 @@ class PortMap:
         out_len = np.zeros(n, np.uint16)
         disp = np.zeros(n, np.uint8)
         st = np.zeros(n, np.uint8)
-        lib().or_nat64_6to4(self.h, _p(arena), _p(off), _p(length), n, _p(out), _p(out_off),
-                            _p(out_len), _p(disp), _p(st))
+        fn(self.h, _p(arena), _p(off), _p(length), n, _p(out), _p(out_off), _p(out_len), _p(disp),
+           _p(st))
         return out, out_len, disp, st
 
     def __del__(self):

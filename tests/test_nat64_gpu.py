@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 import torch
 
+import nat64_replies
 import oracle_lib
 from capsule_amd import _native as N
 from capsule_amd import synth
@@ -168,3 +169,74 @@ def test_packed_output_slots_do_not_clobber(ctx):
     g = out_arena.cpu().numpy()
     bad = np.nonzero(g != o_out)[0]
     assert not len(bad), f"output arena differs at {bad[:8]}"
+
+
+# ---- 4to6 (examples/nat64/main.rs:86-118) ------------------------------------
+def _run_4to6(ctx, gw, pm, frames, shift=0):
+    from capsule_amd import packets
+
+    arena, off, ln = synth.pack_frames(frames, slot=64)
+    out_off = (np.cumsum(np.concatenate([[0], ln.astype(np.int64)[:-1] + 20])) + shift).astype(np.uint32)
+    size = int(out_off[-1]) + int(ln[-1]) + 20 + 8
+    o_out, o_len, o_disp, o_st = pm.nat_4to6(arena, off, ln, out_off, size)
+    out_arena = torch.zeros(size, dtype=torch.uint8, device=DEV)
+    ob, disp, st = gw.nat_4to6(packets.PacketBatch.from_numpy(arena, off, ln, DEV), out_arena,
+                               torch.from_numpy(out_off.view(np.int32)).to(DEV))
+    torch.cuda.synchronize()
+    g_disp, g_st = disp.cpu().numpy(), st.cpu().numpy()
+    bad = np.nonzero(g_disp != o_disp)[0]
+    assert not len(bad), f"4to6 disposition differs at {bad[:8]}: {g_disp[bad[:4]]} vs {o_disp[bad[:4]]}"
+    bad = np.nonzero(g_st != o_st)[0]
+    assert not len(bad), f"4to6 status differs at {bad[:8]}: {g_st[bad[:4]]} vs {o_st[bad[:4]]}"
+    assert (ob.len.cpu().numpy().view(np.uint16) == o_len).all()
+    g_out = out_arena.cpu().numpy()
+    bad = np.nonzero(g_out != o_out)[0]
+    assert not len(bad), f"4to6 output arena differs at bytes {bad[:8]}"
+    return o_out, o_len, o_disp, out_off
+
+
+@pytest.mark.parametrize("shift", [0, 2])
+def test_4to6_parity_after_6to4(ctx, shift):
+    from capsule_amd import packets
+
+    rng = np.random.default_rng(41 + shift)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=14)
+    pm = oracle_lib.PortMap()
+    a, o, l = synth.nat64_stream(6000, n_keys=900, seed=42, drop_frac=0.05)
+    o_out, o_len, o_disp, _ = pm.nat_6to4(a, o, l)
+    gw.nat_6to4(packets.PacketBatch.from_numpy(a, o, l, DEV))
+    torch.cuda.synchronize()
+    frames = nat64_replies.replies(o_out, o, o_len, o_disp, rng)
+    out, olen, disp, out_off = _run_4to6(ctx, gw, pm, frames, shift)
+    assert {N.ACT, N.DROP, N.ABORT} <= set(disp.tolist())
+
+
+def test_4to6_round_trip_properties(ctx):
+    """6to4 then 4to6 of the replies: every reply goes back to the original
+    IPv6 source and TCP port, from 64:ff9b::<v4 src>, with valid checksums."""
+    import struct
+
+    from capsule_amd import packets
+
+    rng = np.random.default_rng(77)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=14)
+    pm = oracle_lib.PortMap()
+    a, o, l = synth.nat64_stream(4000, n_keys=500, seed=43)
+    o_out, o_len, o_disp, _ = pm.nat_6to4(a, o, l)
+    gw.nat_6to4(packets.PacketBatch.from_numpy(a, o, l, DEV))
+    torch.cuda.synchronize()
+    frames = nat64_replies.replies(o_out, o, o_len, o_disp, rng, junk=0.0)
+    out, olen, disp, out_off = _run_4to6(ctx, gw, pm, frames)
+    assert (disp == N.ACT).all()
+    back = [bytes(out[int(s) : int(s) + int(n)]) for s, n in zip(out_off, olen)]
+    arena, off, ln = synth.pack_frames(back)
+    meta, _, _, fl = oracle_lib.parse_batch(arena, off, ln, 0x7F, fields=True)
+    assert (meta & 0xFF == 0).all() and (meta & N.META_L4_CSUM_OK).all()
+    rec = fl.view(np.dtype(N.HDR_RECORD_FIELDS)).reshape(-1)
+    src = a.reshape(-1, 256)[:, 22:38]
+    sport = a.reshape(-1, 256)[:, 54:56]
+    for j, fr in enumerate(frames):  # the j-th reply answers the j-th 6to4 frame
+        assert bytes(rec["dst_ip"][j]) == bytes(src[j])
+        assert int(rec["dst_port"][j]) == int.from_bytes(bytes(sport[j]), "big")
+        k = {0x8100: 1, 0x88A8: 2}.get(int.from_bytes(fr[12:14], "big"), 0)
+        assert bytes(rec["src_ip"][j]) == bytes.fromhex("0064ff9b0000000000000000") + fr[26 + 4 * k : 30 + 4 * k]

@@ -90,3 +90,50 @@ def test_oracle_under_sanitizers():
     r = subprocess.run([sys.executable, "-c", code], cwd=str(oracle_lib.ROOT), env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "clean" in r.stdout, r.stderr[-2000:]
+
+
+def test_oracle_nat64_4to6_drops_unknown_ports():
+    """4to6 before any 6to4: ADDR_MAP is empty, every TCP frame is DROP
+    (examples/nat64/main.rs:113-114); non-IPv4 frames ABORT."""
+    a, o, l = synth.uniform(200, kind=synth.V4_TCP, frame_len=128, seed=5)
+    pm = oracle_lib.PortMap()
+    out, olen, disp, st = pm.nat_4to6(a, o, l, o + np.uint32(0), len(a) + 64)
+    tcp_ok = disp != N.ABORT
+    assert (disp[tcp_ok] == N.DROP).all()
+    a6, o6, l6 = synth.uniform(50, kind=synth.V6_TCP, frame_len=128, seed=6)
+    _, _, disp6, st6 = pm.nat_4to6(a6, o6, l6, o6, len(a6) + 64)
+    assert (disp6 == N.ABORT).all() and (st6 == N.PKT["NOT_IPV4"]).all()
+
+
+def test_oracle_nat64_round_trip():
+    """6to4 then 4to6 of reply frames in the oracle alone: each reply goes back
+    to the original v6 source / port from 64:ff9b::<v4 src>, checksums valid."""
+    import nat64_replies
+
+    rng = np.random.default_rng(3)
+    pm = oracle_lib.PortMap()
+    a, o, l = synth.nat64_stream(500, n_keys=80, seed=9)
+    out, olen, disp, _ = pm.nat_6to4(a, o, l)
+    assert (disp == N.ACT).all()
+    frames = nat64_replies.replies(out, o, olen, disp, rng, junk=0.0)
+    ra, ro, rl = synth.pack_frames(frames)
+    out_off = (ro + np.arange(len(ro), dtype=np.uint64) * 64).astype(np.uint32)
+    back, blen, bdisp, _ = pm.nat_4to6(ra, ro, rl, out_off, len(ra) + 64 * len(ro) + 64)
+    assert (bdisp == N.ACT).all() and (blen == rl + 20).all()
+    fr = [bytes(back[int(s):int(s) + int(n)]) for s, n in zip(out_off, blen)]
+    ba, bo, bl = synth.pack_frames(fr)
+    meta, _, _, fl = oracle_lib.parse_batch(ba, bo, bl, 0x7F, fields=True)
+    assert (meta & 0xFF == 0).all() and (meta & N.META_L4_CSUM_OK).all()
+    rec = fl.view(np.dtype(N.HDR_RECORD_FIELDS)).reshape(-1)
+    a2 = a.reshape(-1, 256)
+    for j, f in enumerate(frames):
+        assert bytes(rec["dst_ip"][j]) == bytes(a2[j, 22:38])
+        assert int(rec["dst_port"][j]) == int.from_bytes(bytes(a2[j, 54:56]), "big")
+        k = {0x8100: 1, 0x88A8: 2}.get(int.from_bytes(f[12:14], "big"), 0)
+        assert bytes(rec["src_ip"][j]) == bytes.fromhex("0064ff9b") + bytes(8) + f[26 + 4 * k:30 + 4 * k]
+    # junk replies: oracle must classify every frame without crashing
+    frames = nat64_replies.replies(out, o, olen, disp, rng, junk=1.0)
+    ra, ro, rl = synth.pack_frames(frames)
+    out_off = (ro + np.arange(len(ro), dtype=np.uint64) * 64).astype(np.uint32)
+    _, _, jd, _ = pm.nat_4to6(ra, ro, rl, out_off, len(ra) + 64 * len(ro) + 64)
+    assert {N.ACT, N.DROP, N.ABORT} <= set(jd.tolist())

@@ -29,13 +29,21 @@ WORKER = textwrap.dedent("""
 """) % (ROOT, os.path.join(ROOT, "tests"))
 
 
+def _free_port():
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
 def test_two_rank_gloo_shards(tmp_path):
     script = tmp_path / "worker.py"
     script.write_text(WORKER)
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(
         [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-         "--master-addr=127.0.0.1", "--master-port=29517", str(script)],
+         "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(script)],
         capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     import json

@@ -49,6 +49,51 @@ __global__ __launch_bounds__(256) void aos_window(const uint8_t *arena, const ui
   out[i] = s[0] ^ s[1] ^ s[2] ^ s[3];
 }
 
+// nat64-shaped data movement: 4 lanes per 256-B frame, 4 x 16-B chunks per
+// lane, output chunk c <- input bytes [16c + SHIFT, 16c + SHIFT + 16).
+template <int SHIFT>
+__global__ __launch_bounds__(256) void copy_frames(const uint8_t *in, uint8_t *out, uint32_t n,
+                                                   uint32_t new_len) {
+  const uint32_t g = threadIdx.x & 3u, p = blockIdx.x * 64u + threadIdx.x / 4u;
+  if (p >= n) return;
+  auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(in), (short)0, (int)(n * 256u), 0x00020000);
+  auto os = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(n * 256u), 0x00020000);
+  u32x4 v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t c = 4u * g + j;
+    v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * c < new_len ? p * 256u + 16u * c + SHIFT : 0xffffff00u), 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t c = 4u * g + j;
+    __builtin_amdgcn_raw_buffer_store_b128(v[j], os, (int)(16u * c + 16u <= new_len ? p * 256u + 16u * c : 0xffffff00u), 0, 0);
+  }
+}
+
+// copy mapping sweep: G lanes per 256-B frame, 16/G chunks per lane, chunk
+// order contiguous per lane (IL=false) or interleaved across the group (IL=true),
+// cache policy AUX on loads and stores.
+template <int G, bool IL, int AUX>
+__global__ __launch_bounds__(256) void copy_map(const uint8_t *in, uint8_t *out, uint32_t n) {
+  constexpr int C = 16 / G;
+  const uint32_t g = threadIdx.x % G, p = blockIdx.x * (256 / G) + threadIdx.x / G;
+  if (p >= n) return;
+  auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(in), (short)0, (int)(n * 256u), 0x00020000);
+  auto os = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(n * 256u), 0x00020000);
+  u32x4 v[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    const uint32_t c = IL ? (uint32_t)j * G + g : g * C + j;
+    v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(p * 256u + 16u * c), 0, AUX);
+  }
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    const uint32_t c = IL ? (uint32_t)j * G + g : g * C + j;
+    __builtin_amdgcn_raw_buffer_store_b128(v[j], os, (int)(p * 256u + 16u * c), 0, AUX);
+  }
+}
+
 static uint32_t lcg(uint64_t &s) {
   s = s * 6364136223846793005ull + 1442695040888963407ull;
   return (uint32_t)(s >> 33);
@@ -146,6 +191,28 @@ int main(int argc, char **argv) {
       cgpu_batch b = {arena[r], bytes, off[r], len[r], n};
       cgpu_parse_out o = {meta, c.csum_out ? csum : nullptr, hash, nullptr};
       if (cgpu_parse_batch(ctx, &b, c.flags, &o, st)) { fprintf(stderr, "parse\n"); exit(2); }
+    });
+  }
+  {  // nat64-shaped copies over 1M x 256-B frames (separate, larger arena)
+    const uint32_t nf = n;
+    uint8_t *fin[4], *fout;
+    for (int r = 0; r < 4; ++r) CK(hipMalloc(&fin[r], (size_t)nf * 256));
+    CK(hipMalloc(&fout, (size_t)nf * 256));
+    for (int r = 0; r < 4; ++r) CK(hipMemset(fin[r], r, (size_t)nf * 256));
+    const double fb = (double)nf * (256 + 240);
+    time_it("copy_frames_shift20_240B", fb, [&](int r) {
+      hipLaunchKernelGGL(copy_frames<20>, dim3((nf + 63) / 64), dim3(256), 0, st, fin[r % 4], fout, nf, 240u);
+    });
+#define MAPCASE(G, IL, AUX)                                                                 \
+  time_it("copy_map_G" #G "_IL" #IL "_aux" #AUX, (double)nf * 512, [&](int r) {               \
+    hipLaunchKernelGGL((copy_map<G, IL, AUX>), dim3((nf * G + 255) / 256), dim3(256), 0, st,  \
+                       fin[r % 4], fout, nf);                                                 \
+  });
+    MAPCASE(1, false, 0) MAPCASE(2, false, 0) MAPCASE(4, false, 0) MAPCASE(4, true, 0)
+    MAPCASE(8, true, 0) MAPCASE(16, true, 0) MAPCASE(16, true, 2) MAPCASE(4, true, 2)
+    MAPCASE(16, true, 1)
+    time_it("copy_frames_shift0_256B", (double)nf * 512, [&](int r) {
+      hipLaunchKernelGGL(copy_frames<0>, dim3((nf + 63) / 64), dim3(256), 0, st, fin[r % 4], fout, nf, 256u);
     });
   }
   cgpu_ctx_destroy(ctx);
