@@ -61,7 +61,34 @@ def make_workload(cfg, seed):
         desc = "1M x 256B IPv6/TCP -> IPv4 6to4 rewrite + TCP/IPv4 checksums (examples/nat64)"
         return dict(arena=arena, off=off, len=ln, flags=0, kind="nat64", desc=desc,
                     algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame="256B")
+    if cfg == "nat64_4to6":
+        # the v6 stream that populates the port map; the timed replies are
+        # built from its 6to4 output on the device (main())
+        arena, off, ln = synth.nat64_stream(n, seed=seed)
+        desc = ("1M x 236B IPv4/TCP replies -> IPv6 4to6 rewrite + TCP checksum "
+                "(examples/nat64), port map populated by a 6to4 pass")
+        return dict(arena=arena, off=off, len=ln, flags=0, kind="nat64_4to6", desc=desc,
+                    frame="236B")
     raise SystemExit(f"unknown config {cfg}")
+
+
+def nat64_4to6_setup(w, ctx, dev):
+    """Run the 6to4 pass (untimed) and turn its output into reply frames."""
+    import torch
+
+    from capsule_amd import packets
+    from capsule_amd import synth
+
+    gw = packets.Nat64Gateway(ctx, capacity_log2=17)
+    b = packets.PacketBatch.from_numpy(w["arena"], w["off"], w["len"], dev)
+    ob, disp, _ = gw.nat_6to4(b)
+    torch.cuda.synchronize(dev)
+    assert (disp.cpu().numpy() == 0).all()
+    w["setup"] = (w["arena"], w["off"], w["len"])
+    w["arena"], w["off"], w["len"] = synth.nat64_replies(
+        ob.arena.cpu().numpy(), w["off"], ob.len.cpu().numpy().view(np.uint16))
+    w["algo_bytes"] = int(w["len"].astype(np.int64).sum()) + 6 * len(w["off"])
+    return gw
 
 
 def imix_header_bytes_workload(seed):
@@ -110,8 +137,12 @@ def cpu_baseline(w, seconds):
         olen = np.zeros(n, np.uint16)
         disp = np.zeros(n, np.uint8)
         st = np.zeros(n, np.uint8)
-        run = lambda: L.or_nat64_6to4(pm.h, p(arena), p(off), p(ln), n, p(out), p(off),  # noqa
-                                      p(olen), p(disp), p(st))
+        fn = L.or_nat64_6to4
+        if w["kind"] == "nat64_4to6":
+            pm.nat_6to4(*w["setup"])  # same port map as the device side
+            fn = L.or_nat64_4to6
+        run = lambda: fn(pm.h, p(arena), p(off), p(ln), n, p(out), p(off),  # noqa
+                         p(olen), p(disp), p(st))
     run()  # warm
     passes, t0 = 0, time.perf_counter()
     while True:
@@ -149,7 +180,7 @@ def main():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="parse64",
-                    choices=["parse64", "imix", "imix_csum", "nat64"])
+                    choices=["parse64", "imix", "imix_csum", "nat64", "nat64_4to6"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--e2e", action="store_true",
@@ -167,10 +198,12 @@ def main():
     g = ShardGroup()
     dev = torch.device("cuda", g.local_rank)
     torch.cuda.set_device(dev)
-    seed = g.shard_seed(0xC0FFEE + {"parse64": 2, "imix": 3, "imix_csum": 3, "nat64": 4}[args.config])
+    seed = g.shard_seed(0xC0FFEE + {"parse64": 2, "imix": 3, "imix_csum": 3, "nat64": 4,
+                                    "nat64_4to6": 4}[args.config])
     w = make_workload(args.config, seed)
     n = len(w["off"])
     ctx = packets.Context(g.local_rank)
+    gw = nat64_4to6_setup(w, ctx, dev) if w["kind"] == "nat64_4to6" else None
 
     # R resident copies so the rotation's footprint exceeds the Infinity Cache
     batch_bytes = len(w["arena"]) + 6 * n
@@ -190,13 +223,14 @@ def main():
         def launch(k):
             launchers[k % (2 * copies)]()
     else:
-        gw = packets.Nat64Gateway(ctx, capacity_log2=17)
+        direction = "4to6" if gw is not None else "6to4"
+        gw = gw or packets.Nat64Gateway(ctx, capacity_log2=17)
         nat_out = [(torch.empty_like(b.arena), b.off, torch.empty(n, dtype=torch.int16, device=dev),
                     torch.empty(n, dtype=torch.uint8, device=dev),
                     torch.empty(n, dtype=torch.uint8, device=dev)) for b in batches[:2]]
 
-        launchers = [packets.Nat64Launcher(gw, batches[k % copies], nat_out[k & 1], stream)
-                     for k in range(2 * copies)]
+        launchers = [packets.Nat64Launcher(gw, batches[k % copies], nat_out[k & 1], stream,
+                                           direction) for k in range(2 * copies)]
 
         def launch(k):
             launchers[k % (2 * copies)]()
@@ -284,6 +318,7 @@ def e2e(args):
     w = make_workload(args.config, 0xC0FFEE + 2)
     n = len(w["off"])
     ctx = packets.Context(0)
+    gw = nat64_4to6_setup(w, ctx, dev) if w["kind"] == "nat64_4to6" else None
     host = dict(arena=torch.from_numpy(w["arena"]).pin_memory(),
                 off=torch.from_numpy(w["off"].view(np.int32)).pin_memory(),
                 len=torch.from_numpy(w["len"].view(np.int16)).pin_memory())
@@ -303,14 +338,15 @@ def e2e(args):
             host_out[d][1].copy_(outs[d].flow_hash, non_blocking=True)
         down_bytes = 12 * n
     else:
-        gw = packets.Nat64Gateway(ctx, capacity_log2=17)
+        direction = "4to6" if gw is not None else "6to4"
+        gw = gw or packets.Nat64Gateway(ctx, capacity_log2=17)
         nat = [(torch.empty_like(bufs[d].arena), bufs[d].off,
                 torch.empty(n, dtype=torch.int16, device=dev),
                 torch.empty(n, dtype=torch.uint8, device=dev),
                 torch.empty(n, dtype=torch.uint8, device=dev)) for d in range(D)]
         host_out = [(torch.empty_like(host["arena"], pin_memory=True),
                      torch.empty(n, dtype=torch.int16, pin_memory=True)) for _ in range(D)]
-        launch = [packets.Nat64Launcher(gw, bufs[d], nat[d], comp) for d in range(D)]
+        launch = [packets.Nat64Launcher(gw, bufs[d], nat[d], comp, direction) for d in range(D)]
 
         def back(d):
             host_out[d][0].copy_(nat[d][0], non_blocking=True)

@@ -43,6 +43,8 @@ F_FLOW_HASH = 1 << 6
 
 ACT, DROP, ABORT = 0, 1, 2
 
+KEY_U8, KEY_META_CLASS = 0, 1
+
 
 def meta_status(m):
     return m & 0xFF
@@ -98,7 +100,7 @@ HDR_RECORD_SIZE = 96
 EXPORTS = [
     "cgpu_ctx_create", "cgpu_ctx_destroy", "cgpu_parse_batch", "cgpu_parse_host",
     "cgpu_portmap_create", "cgpu_portmap_destroy", "cgpu_portmap_next_port",
-    "cgpu_portmap_size", "cgpu_nat64_6to4", "cgpu_nat64_4to6", "cgpu_last_error", "cgpu_strerror",
+    "cgpu_portmap_size", "cgpu_nat64_6to4", "cgpu_nat64_4to6", "cgpu_group_by", "cgpu_last_error", "cgpu_strerror",
     "cgpu_pkt_status_str", "cgpu_abi_version",
 ]
 
@@ -143,6 +145,8 @@ def lib():
     L.cgpu_nat64_6to4.argtypes = [vp, vp, P(Batch), vp, ctypes.c_uint64, vp, vp, vp, vp, vp]
     L.cgpu_nat64_4to6.restype = i32
     L.cgpu_nat64_4to6.argtypes = [vp, vp, P(Batch), vp, ctypes.c_uint64, vp, vp, vp, vp, vp]
+    L.cgpu_group_by.restype = i32
+    L.cgpu_group_by.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp]
     if L.cgpu_abi_version() != ABI_VERSION:
         raise RuntimeError("capsule_amd: libcapsule_gpu.so ABI version mismatch")
     _lib = L

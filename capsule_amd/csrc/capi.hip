@@ -44,6 +44,8 @@ struct cgpu_ctx {
   size_t arena_cap = 0;
   uint8_t *h_desc = nullptr, *d_desc = nullptr;  // off[n] | len[n] | outputs
   size_t desc_cap = 0;
+  uint32_t *gb_counts = nullptr;  // cgpu_group_by scratch
+  size_t gb_cap = 0;              // entries
 };
 
 struct cgpu_portmap {
@@ -122,6 +124,7 @@ void cgpu_ctx_destroy(cgpu_ctx *c) {
   if (c->d_arena) (void)hipFree(c->d_arena);
   if (c->h_desc) (void)hipHostFree(c->h_desc);
   if (c->d_desc) (void)hipFree(c->d_desc);
+  if (c->gb_counts) (void)hipFree(c->gb_counts);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -364,6 +367,40 @@ int cgpu_nat64_4to6(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8
                     uint8_t *disposition, uint8_t *status, void *stream) {
   return nat64_call(false, ctx, pm, in, out_arena, out_arena_len, out_off, out_len, disposition,
                     status, stream);
+}
+
+int cgpu_group_by(cgpu_ctx *ctx, const void *key, uint32_t key_kind, uint32_t n,
+                  uint32_t n_groups, uint32_t *idx, uint32_t *group_off, void *stream) {
+  if (!ctx || !group_off || n_groups < 1 || n_groups > 64) return fail(CGPU_EINVAL);
+  if (key_kind != CGPU_KEY_U8 && key_kind != CGPU_KEY_META_CLASS) return fail(CGPU_EINVAL);
+  if (n > (1u << 28)) return fail(CGPU_EINVAL);
+  if (n == 0) {
+    if (hipMemsetAsync(group_off, 0, 4ull * (n_groups + 1), (hipStream_t)stream) != hipSuccess)
+      return fail(CGPU_EIO);
+    return ok();
+  }
+  if (!key || !idx) return fail(CGPU_EINVAL);
+  const uint32_t tiles = cgpu::group_by_tiles(n);
+  const size_t need = (size_t)tiles * n_groups;
+  if (ctx->gb_cap < need) {
+    if (ctx->gb_counts) (void)hipFree(ctx->gb_counts);
+    ctx->gb_counts = nullptr;
+    ctx->gb_cap = 0;
+    if (hipMalloc(&ctx->gb_counts, 4 * need) != hipSuccess) return fail(CGPU_ENOMEM);
+    ctx->gb_cap = need;
+  }
+  cgpu::GroupByArgs a;
+  a.key = key;
+  a.kind = key_kind;
+  a.n = n;
+  a.groups = n_groups;
+  a.tiles = tiles;
+  a.counts = ctx->gb_counts;
+  a.idx = idx;
+  a.group_off = group_off;
+  hipError_t e = cgpu::launch_group_by(a, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e);
+  return ok();
 }
 
 }  // extern "C"

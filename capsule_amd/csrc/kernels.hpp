@@ -76,4 +76,19 @@ hipError_t launch_nat64_4to6(const Nat64Args &a, hipStream_t s);
 hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStream_t s);
 uint32_t nat64_num_blocks(uint32_t n);
 
+// ---- group_by --------------------------------------------------------------
+struct GroupByArgs {
+  const void *key;     // u8 arm keys or u32 meta words (kind)
+  uint32_t kind;       // CGPU_KEY_*
+  uint32_t n;
+  uint32_t groups;     // arms, the last one is the catch-all (1..64)
+  uint32_t tiles;      // group_by_tiles(n)
+  uint32_t *counts;    // scratch [groups * tiles]
+  uint32_t *idx;       // [n] packet indices grouped by arm
+  uint32_t *group_off; // [groups + 1]
+};
+
+uint32_t group_by_tiles(uint32_t n);
+hipError_t launch_group_by(const GroupByArgs &a, hipStream_t s);
+
 }  // namespace cgpu

@@ -214,6 +214,54 @@ def parse_host(ctx, frames, flags=None, fields=False):
     return meta, csum, fh, recs
 
 
+class Groups:
+    """Result of `group_by`: `idx[off[k]:off[k+1]]` are arm k's packets."""
+
+    def __init__(self, idx, off):
+        self.idx = idx
+        self.off = off
+
+    def arm(self, k, host_off=None):
+        o = host_off if host_off is not None else self.off.cpu().tolist()
+        return self.idx[o[k]:o[k + 1]]
+
+    def counts(self):
+        o = self.off.cpu().tolist()
+        return [o[k + 1] - o[k] for k in range(len(o) - 1)]
+
+
+# arms of group_by(..., by="class") (include/capsule_gpu.h CGPU_KEY_META_CLASS)
+CLASS_ARMS = ("v4_udp", "v4_tcp", "v6_udp", "v6_tcp", "other")
+
+
+def group_by(ctx, key, n_groups=None, by="key", idx=None, stream=None):
+    """`batch.group_by(selector, compose!{..})` (core/src/batch/group_by.rs:
+    143-172) over a whole burst: a stable partition of packet indices into
+    arms.  `by="key"`: `key` is a u8 tensor of arm numbers (e.g. a nat64
+    disposition array, whose arm sizes are the Emitted/Dropped/Aborted
+    counters of send.rs:104-110); keys >= n_groups - 1 fall into the last,
+    catch-all arm.  `by="class"`: `key` is the parse meta tensor and the arms
+    are CLASS_ARMS.  Asynchronous on `stream`."""
+    n = key.numel()
+    if by == "class":
+        kind, n_groups = N.KEY_META_CLASS, n_groups or len(CLASS_ARMS)
+        if key.dtype != torch.int32:
+            raise TypeError("group_by(by='class') takes the int32 parse meta tensor")
+    elif by == "key":
+        kind = N.KEY_U8
+        if key.dtype != torch.uint8 or n_groups is None:
+            raise TypeError("group_by(by='key') takes a uint8 key tensor and n_groups")
+    else:
+        raise ValueError(by)
+    if idx is None:
+        idx = torch.empty(n, dtype=torch.int32, device=key.device)
+    off = torch.empty(n_groups + 1, dtype=torch.int32, device=key.device)
+    rc = N.lib().cgpu_group_by(ctx.handle, _ptr(key.contiguous()), kind, n, n_groups, _ptr(idx),
+                               _ptr(off), _stream_handle(stream))
+    N.check(rc, "cgpu_group_by")
+    return Groups(idx[:n], off)
+
+
 class Nat64Gateway:
     """examples/nat64 6to4 direction with its PORT_MAP on the device.
 
@@ -313,13 +361,15 @@ class ParseLauncher:
 
 
 class Nat64Launcher:
-    """A `Nat64Gateway.nat_6to4` call with prebuilt ctypes arguments."""
+    """A `Nat64Gateway.nat_6to4` (or `nat_4to6`) call with prebuilt ctypes
+    arguments."""
 
-    def __init__(self, gw, batch, out, stream=None):
+    def __init__(self, gw, batch, out, stream=None, direction="6to4"):
         out_arena, out_off, out_len, disp, status = out
         self._keep = (gw, batch, out)
         self._cb = batch.cbatch()
-        self._fn = N.lib().cgpu_nat64_6to4
+        self._name = {"6to4": "cgpu_nat64_6to4", "4to6": "cgpu_nat64_4to6"}[direction]
+        self._fn = getattr(N.lib(), self._name)
         self._args = [gw.ctx.handle, gw._h, ctypes.byref(self._cb), _ptr(out_arena),
                       out_arena.numel(), _ptr(out_off), _ptr(out_len), _ptr(disp), _ptr(status),
                       _stream_handle(stream)]
@@ -327,4 +377,4 @@ class Nat64Launcher:
     def __call__(self):
         rc = self._fn(*self._args)
         if rc:
-            N.check(rc, "cgpu_nat64_6to4")
+            N.check(rc, self._name)

@@ -275,3 +275,22 @@ def fuzz(n, seed=1, max_len=1600):
         arena[int(off[i]) : int(off[i]) + len(fr)] = np.frombuffer(fr, np.uint8)
     lens = np.array([len(f) for f in frames], np.uint16)
     return arena, off.astype(np.uint32), lens
+
+
+def nat64_replies(out_arena, off, out_len):
+    """IPv4/TCP replies to untagged 6to4 output frames, for the 4to6 rewrite.
+
+    Swapping the IPv4 addresses and the TCP ports turns each output frame
+    into the peer's answer, sent to the gateway port the port map assigned;
+    both checksums are sums over the swapped words, so they stay valid.
+    Frames keep their offsets and lengths (nat_4to6 makes them 20 B longer,
+    so the slot must leave that room).
+    """
+    a = np.array(out_arena, dtype=np.uint8, copy=True)
+    o = off.astype(np.int64)
+    assert (a[o + 12] == 0x08).all() and (a[o + 13] == 0x00).all(), "untagged IPv4 frames"
+    for lo, hi, w in ((26, 30, 4), (34, 36, 2)):
+        i = o[:, None] + np.arange(w)[None, :]
+        x, y = a[i + lo].copy(), a[i + hi].copy()
+        a[i + lo], a[i + hi] = y, x
+    return a, off.astype(np.uint32), out_len.astype(np.uint16)

@@ -224,6 +224,26 @@ int cgpu_nat64_4to6(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in,
                     uint8_t *out_arena, uint64_t out_arena_len, const uint32_t *out_off,
                     uint16_t *out_len, uint8_t *disposition, uint8_t *status, void *stream);
 
+/* ---- group_by (core/src/batch/group_by.rs:143-172) -----------------------
+ * Stable partition of a batch's packet indices by a per-packet arm key: the
+ * device form of `batch.group_by(selector, compose!{...})`.  Arm k (k <
+ * n_groups - 1) receives the packets whose key is k, in batch order; every
+ * other key goes to the last arm, the catch-all (`_ =>` / the implicit
+ * pass-through arm of compose!, group_by.rs:186-200).  The per-arm counts
+ * double as the disposition counters of send.rs:104-110 when the key is a
+ * cgpu_disposition array.
+ *   key_kind CGPU_KEY_U8:         key = const uint8_t[n] (e.g. disposition)
+ *   key_kind CGPU_KEY_META_CLASS: key = const uint32_t[n] parse meta words;
+ *     arm = 0 v4/UDP, 1 v4/TCP, 2 v6/UDP, 3 v6/TCP, 4 status != OK
+ * idx[n]: packet indices grouped by arm; group_off[n_groups + 1]: arm k owns
+ * idx[group_off[k] .. group_off[k+1]).  n_groups in 1..64, n <= 2^28.  All
+ * device pointers; asynchronous on `stream`.  Uses per-context scratch: one
+ * stream at a time per context (one context per core thread, as everywhere). */
+#define CGPU_KEY_U8 0u
+#define CGPU_KEY_META_CLASS 1u
+int cgpu_group_by(cgpu_ctx *ctx, const void *key, uint32_t key_kind, uint32_t n,
+                  uint32_t n_groups, uint32_t *idx, uint32_t *group_off, void *stream);
+
 /* ---- errors -------------------------------------------------------------- */
 int cgpu_last_error(void);
 const char *cgpu_strerror(int code);

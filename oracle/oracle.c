@@ -640,3 +640,46 @@ void or_nat64_6to4(or_portmap *pm, const uint8_t *arena, const uint32_t *off, co
   }
   free(m);
 }
+
+/* ---- group_by (core/src/batch/group_by.rs) ------------------------------ */
+
+/* The selector of the CGPU_KEY_META_CLASS arms: a match on the typed parse
+ * result a pipeline would write as its group_by closure. */
+static uint32_t meta_class(uint32_t m) {
+  if ((m & 0xffu) != CGPU_PKT_OK) return 4;
+  const uint32_t l3 = (m >> 16) & 3u, l4 = (m >> 18) & 3u;
+  if (l3 == CGPU_L3_IPV4) return l4 == CGPU_L4_TCP ? 1 : 0;
+  return l4 == CGPU_L4_TCP ? 3 : 2;
+}
+
+/* GroupBy::next (group_by.rs:143-172): for each packet in arrival order,
+ * `groups.get_mut(&key)` or the catch-all, then the arm runs the packet.
+ * Each arm's packets are collected in a growable list, like the fanout
+ * queue, and concatenated arm by arm. */
+void or_group_by(const void *key, uint32_t key_kind, uint32_t n, uint32_t n_groups, uint32_t *idx,
+                 uint32_t *group_off) {
+  uint32_t **arm = (uint32_t **)calloc(n_groups, sizeof(uint32_t *));
+  uint32_t *cnt = (uint32_t *)calloc(n_groups, sizeof(uint32_t));
+  uint32_t *cap = (uint32_t *)calloc(n_groups, sizeof(uint32_t));
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t k = key_kind == CGPU_KEY_META_CLASS ? meta_class(((const uint32_t *)key)[i])
+                                                  : ((const uint8_t *)key)[i];
+    if (k >= n_groups - 1) k = n_groups - 1; /* None => catchall */
+    if (cnt[k] == cap[k]) {
+      cap[k] = cap[k] ? 2 * cap[k] : 16;
+      arm[k] = (uint32_t *)realloc(arm[k], cap[k] * sizeof(uint32_t));
+    }
+    arm[k][cnt[k]++] = i;
+  }
+  uint32_t at = 0;
+  for (uint32_t k = 0; k < n_groups; ++k) {
+    group_off[k] = at;
+    if (cnt[k]) memcpy(idx + at, arm[k], cnt[k] * sizeof(uint32_t));
+    at += cnt[k];
+    free(arm[k]);
+  }
+  group_off[n_groups] = at;
+  free(arm);
+  free(cnt);
+  free(cap);
+}

@@ -65,6 +65,12 @@ void or_nat64_4to6(or_portmap *pm, const uint8_t *arena, const uint32_t *off, co
                    uint32_t n, uint8_t *out_arena, const uint32_t *out_off, uint16_t *out_len,
                    uint8_t *disposition, uint8_t *status);
 
+/* core/src/batch/group_by.rs:143-172 over a burst: packets visited in
+ * order, each appended to the arm its key selects (catch-all = last arm).
+ * key_kind / arms as cgpu_group_by.                                      */
+void or_group_by(const void *key, uint32_t key_kind, uint32_t n, uint32_t n_groups, uint32_t *idx,
+                 uint32_t *group_off);
+
 #ifdef __cplusplus
 }
 #endif

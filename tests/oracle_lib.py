@@ -50,6 +50,8 @@ def load(name="liboracle.so"):
     L.or_portmap_size.argtypes = [vp]
     L.or_nat64_6to4.restype = None
     L.or_nat64_6to4.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
+    L.or_group_by.restype = None
+    L.or_group_by.argtypes = [vp, u32, u32, u32, vp, vp]
     L.or_nat64_4to6.restype = None
     L.or_nat64_4to6.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
     return L
@@ -82,6 +84,16 @@ def parse_batch(arena, off, length, flags, fields=True):
     lib().or_parse_batch(_p(arena), _p(off), _p(length), n, flags, _p(meta), _p(csum), _p(h),
                          _p(fl))
     return meta, csum, h, fl
+
+
+def group_by(key, n_groups, kind=0):
+    """Oracle group_by -> (idx u32[n], group_off u32[n_groups + 1])."""
+    key = np.ascontiguousarray(key)
+    n = len(key)
+    idx = np.zeros(n, np.uint32)
+    off = np.zeros(n_groups + 1, np.uint32)
+    lib().or_group_by(_p(key), kind, n, n_groups, _p(idx), _p(off))
+    return idx, off
 
 
 class PortMap:

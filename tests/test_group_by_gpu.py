@@ -1,0 +1,83 @@
+"""Parity of cgpu_group_by (device stable partition) with the oracle's
+restatement of GroupBy::next (core/src/batch/group_by.rs:143-172): arm
+contents in batch order, catch-all arm, arm offsets, for u8 keys and for
+parse-meta classes."""
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib
+from capsule_amd import _native as N
+from capsule_amd import synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _check(ctx, key, n_groups, kind):
+    from capsule_amd import packets
+
+    t = torch.from_numpy(key.view(np.int32) if kind else key).to(DEV)
+    g = packets.group_by(ctx, t, n_groups, by="class" if kind else "key")
+    torch.cuda.synchronize()
+    idx, off = oracle_lib.group_by(key, n_groups, kind)
+    assert (g.off.cpu().numpy().view(np.uint32) == off).all()
+    assert (g.idx.cpu().numpy().view(np.uint32) == idx).all()
+    return off
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 1000, 1024, 1025, 4097, 300_001])
+@pytest.mark.parametrize("n_groups", [1, 2, 3, 5, 64])
+def test_group_by_u8_keys(ctx, n, n_groups):
+    rng = np.random.default_rng(n * 131 + n_groups)
+    key = rng.integers(0, n_groups + 3, n, dtype=np.uint8)  # some keys name no arm
+    _check(ctx, key, n_groups, N.KEY_U8)
+
+
+def test_group_by_skewed_and_uniform_keys(ctx):
+    rng = np.random.default_rng(5)
+    n = 1 << 20
+    for key in (np.zeros(n, np.uint8), np.full(n, 255, np.uint8),
+                (rng.random(n) < 0.01).astype(np.uint8),
+                rng.integers(0, 64, n, dtype=np.uint8),
+                np.repeat(rng.integers(0, 6, n // 997 + 1, dtype=np.uint8), 997)[:n]):
+        _check(ctx, key, 64 if key.max() > 5 else 6, N.KEY_U8)
+
+
+def test_group_by_parse_class(ctx):
+    """group_by over the parse results: v4/UDP, v4/TCP, v6/UDP, v6/TCP arms
+    plus the error arm, on an IMIX batch with fuzzed frames mixed in."""
+    from capsule_amd import packets
+
+    a, o, l = synth.imix(50_000, vlan_frac=0.1, seed=3)
+    r = packets.parse(ctx, packets.PacketBatch.from_numpy(a, o, l, DEV),
+                      N.F_ACCEPT_ALL | N.F_FLOW_HASH)
+    torch.cuda.synchronize()
+    meta = r.meta.cpu().numpy().view(np.uint32)
+    off = _check(ctx, meta, 5, N.KEY_META_CLASS)
+    assert (np.diff(off.astype(np.int64)) > 0).sum() >= 4
+    fa, fo, fl = synth.fuzz(20_000, seed=4)
+    r = packets.parse(ctx, packets.PacketBatch.from_numpy(fa, fo, fl, DEV),
+                      N.F_ACCEPT_V4 | N.F_ACCEPT_UDP)
+    torch.cuda.synchronize()
+    meta = r.meta.cpu().numpy().view(np.uint32)
+    for groups in (2, 5, 64):
+        _check(ctx, meta, groups, N.KEY_META_CLASS)
+
+
+def test_group_by_nat64_dispositions(ctx):
+    """Send::run (batch/send.rs:95-118) on a nat64 burst: the Act arm is the
+    tx list, arm sizes are the emitted / dropped / aborted counters."""
+    from capsule_amd import packets
+
+    a, o, l = synth.nat64_stream(30_000, n_keys=400, drop_frac=0.1)
+    l[::97] = 30  # truncated frames abort
+    gw = packets.Nat64Gateway(ctx, capacity_log2=12)
+    ob, disp, st = gw.nat_6to4(packets.PacketBatch.from_numpy(a, o, l, DEV))
+    g = packets.group_by(ctx, disp, 3)
+    torch.cuda.synchronize()
+    d = disp.cpu().numpy()
+    assert g.counts() == [int((d == k).sum()) for k in range(3)]
+    assert all(c > 0 for c in g.counts())
+    assert (g.arm(N.ACT).cpu().numpy() == np.nonzero(d == N.ACT)[0]).all()
+    gw.close()

@@ -137,3 +137,14 @@ def test_oracle_nat64_round_trip():
     out_off = (ro + np.arange(len(ro), dtype=np.uint64) * 64).astype(np.uint32)
     _, _, jd, _ = pm.nat_4to6(ra, ro, rl, out_off, len(ra) + 64 * len(ro) + 64)
     assert {N.ACT, N.DROP, N.ABORT} <= set(jd.tolist())
+
+
+def test_oracle_group_by_is_stable_partition():
+    rng = np.random.default_rng(8)
+    for n, g in ((0, 3), (1, 1), (5000, 4), (5000, 64)):
+        key = rng.integers(0, 70, n, dtype=np.uint8)
+        idx, off = oracle_lib.group_by(key, g)
+        arm = np.minimum(key, g - 1)
+        ref = np.argsort(arm, kind="stable")
+        assert (idx == ref).all()
+        assert (off == np.concatenate([[0], np.cumsum(np.bincount(arm, minlength=g))])).all()
