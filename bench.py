@@ -264,7 +264,7 @@ def main():
         from summarize_prof import source_hash
 
         p = json.loads(pmc.read_text())
-        if p.get("src_hash") == source_hash() and "traffic_bytes" in p:
+        if p.get("src_hash") == source_hash(args.config) and "traffic_bytes" in p:
             traffic = int(p["traffic_bytes"])
 
     total_pkts = g.sum(n * args.steps)

@@ -55,9 +55,11 @@ struct cgpu_portmap {
   // per-call scratch
   uint32_t *pkt_slot = nullptr;
   uint32_t *block_sums = nullptr;
-  void *rec_h = nullptr;  // K1 -> K5 header records
+  void *rec_h = nullptr;  // deferred frames' header records
   void *rec_b = nullptr;
+  uint32_t *defer = nullptr;
   uint32_t scratch_n = 0;
+  uint32_t calls = 0;  // 6to4 calls: parity of the deferred-list counter
 };
 
 extern "C" {
@@ -324,12 +326,14 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
     void *m = nullptr;
     const size_t o_sums = align_up(4ull * in->n, 256);
     const size_t o_rech = o_sums + align_up(4ull * nb, 256);
-    const size_t o_recb = o_rech + align_up(48ull * in->n, 256);
-    if (hipMalloc(&m, o_recb + 8ull * in->n + 256) != hipSuccess) return fail(CGPU_ENOMEM);
+    const size_t o_recb = o_rech + align_up(16ull * in->n, 256);
+    const size_t o_defer = o_recb + align_up(8ull * in->n, 256);
+    if (hipMalloc(&m, o_defer + 4ull * in->n + 256) != hipSuccess) return fail(CGPU_ENOMEM);
     pm->pkt_slot = (uint32_t *)m;
     pm->block_sums = (uint32_t *)((uint8_t *)m + o_sums);
     pm->rec_h = (uint8_t *)m + o_rech;
     pm->rec_b = (uint8_t *)m + o_recb;
+    pm->defer = (uint32_t *)((uint8_t *)m + o_defer);
     pm->scratch_n = in->n;
   }
   cgpu::Nat64Args a;
@@ -348,10 +352,13 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   a.block_sums = pm->block_sums;
   a.rec_h = (cgpu::u32x4 *)pm->rec_h;
   a.rec_b = (uint2 *)pm->rec_b;
+  a.defer = pm->defer;
+  a.par = pm->calls & 1u;
   a.pm = pm->dev;
   hipError_t e = to4 ? cgpu::launch_nat64_6to4(a, (hipStream_t)stream)
                      : cgpu::launch_nat64_4to6(a, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e);
+  if (to4) ++pm->calls;
   return ok();
 }
 

@@ -47,7 +47,7 @@ struct PortSlot {
 struct PortMapDev {
   PortSlot *slots;  // [cap]
   uint64_t *rev;    // [65536]: (first ordinal << 32 | slot), ~0 = none (ADDR_MAP, main.rs:38)
-  uint32_t *state;  // [4]: next_port, entries, batch_base, batch_new
+  uint32_t *state;  // [6]: next_port, entries, batch_base, batch_new, deferred[2]
   uint32_t cap_mask;
 };
 
@@ -65,9 +65,10 @@ struct Nat64Args {
   uint8_t *status;
   uint32_t *pkt_slot;    // scratch [n]: table slot (or 0xffffffff)
   uint32_t *block_sums;  // scratch [nblocks + 1]
-  u32x4 *rec_h;          // scratch [3n]: new IPv4 header dwords 0..3 (6to4) or the
-                         // IPv6 header + port + pseudo-header sum, 48 B (4to6)
-  uint2 *rec_b;          // scratch [n]: header dword 4, eth_len | k << 8 | new_len << 16
+  u32x4 *rec_h;          // scratch [n]: deferred 6to4 frames' IPv4 header dwords 0..3
+  uint2 *rec_b;          // scratch [n]: header dword 4, VLAN depth
+  uint32_t *defer;       // scratch [n]: indices of the deferred 6to4 frames
+  uint32_t par;          // call parity: selects the deferred-list counter state[4 + par]
   PortMapDev pm;
 };
 

@@ -20,11 +20,18 @@ import sys
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 
 
-def source_hash():
+# the sources whose code a config's kernels are built from
+_CONFIG_SOURCES = {"parse": ["parse.hip"], "nat64": ["nat64.hip"]}
+
+
+def source_hash(config="parse64"):
+    """Hash of the kernel sources a config runs (shared headers included)."""
+    fam = "nat64" if config.startswith("nat64") else "parse"
     h = hashlib.sha256()
-    for p in sorted((ROOT / "capsule_amd" / "csrc").glob("*.[hc]*")):
-        h.update(p.name.encode())
-        h.update(p.read_bytes())
+    csrc = ROOT / "capsule_amd" / "csrc"
+    for name in sorted(_CONFIG_SOURCES[fam] + ["device_common.hpp", "kernels.hpp"]):
+        h.update(name.encode())
+        h.update((csrc / name).read_bytes())
     h.update((ROOT / "include" / "capsule_gpu.h").read_bytes())
     return h.hexdigest()[:16]
 
@@ -39,7 +46,7 @@ def main():
     kernel = top["Name"]
     out = {"config": config, "kernel": kernel, "calls": int(top["Calls"]),
            "avg_ns": float(top["AverageNs"]), "min_ns": float(top["MinNs"]),
-           "src_hash": source_hash()}
+           "src_hash": source_hash(config)}
     for name, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         f = next(src.glob(f"{name}/*counter_collection.csv"), None)
         if f is None:
