@@ -23,8 +23,10 @@ WORKER = textwrap.dedent("""
         time.sleep(0.01 * (g.rank + 1))
     t = g.timed(step, 3)
     total = g.sum(len(o))
-    print(json.dumps({"rank": g.rank, "seed": seed, "t": t, "total": total,
-                      "h0": int(h[0]), "ok": bool((meta & 0xff == 0).all())}))
+    # one file per rank: two ranks printing to a shared stdout can interleave
+    with open(sys.argv[1] + "/rank%%d.json" %% g.rank, "w") as f:
+        json.dump({"rank": g.rank, "seed": seed, "t": t, "total": total,
+                   "h0": int(h[0]), "ok": bool((meta & 0xff == 0).all())}, f)
     g.close()
 """) % (ROOT, os.path.join(ROOT, "tests"))
 
@@ -43,11 +45,12 @@ def test_two_rank_gloo_shards(tmp_path):
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(
         [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-         "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(script)],
+         "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(script),
+         str(tmp_path)],
         capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     import json
-    rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    rows = [json.loads((tmp_path / f"rank{i}.json").read_text()) for i in range(2)]
     assert len(rows) == 2
     a, b = sorted(rows, key=lambda x: x["rank"])
     assert a["seed"] != b["seed"] and a["h0"] != b["h0"]   # independent shards
