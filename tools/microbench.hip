@@ -49,6 +49,48 @@ __global__ __launch_bounds__(256) void aos_window(const uint8_t *arena, const ui
   out[i] = s[0] ^ s[1] ^ s[2] ^ s[3];
 }
 
+// AoS with a cache policy on the loads (AUX: 1 = glc, 2 = slc, 3 = both)
+template <int AUX>
+__global__ __launch_bounds__(256) void aos_window_aux(const uint8_t *arena, const uint32_t *off,
+                                                      uint32_t n, uint32_t *out) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(arena), (short)0, (int)(n * 64u), 0x00020000);
+  const uint32_t o = off[i];
+  u32x4 s = {0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) s += __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(o + 16u * c), 0, AUX);
+  out[i] = s[0] ^ s[1] ^ s[2] ^ s[3];
+}
+
+// LDS staging: the wave loads the 4 KiB span of its 64 packets coalesced
+// (lane L, instruction c -> bytes 1024c + 16L), writes it to LDS with the
+// 16-B chunk index XOR-swizzled by bits 8-9, then each lane reads its own 64 B.
+__device__ __forceinline__ uint32_t swz(uint32_t a) { return a ^ (((a >> 8) & 3u) << 4); }
+
+__global__ __launch_bounds__(256) void lds_window(const uint8_t *arena, const uint32_t *off,
+                                                  uint32_t n, uint32_t *out) {
+  __shared__ u32x4 lds[4][256];
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(arena), (short)0, (int)(n * 64u), 0x00020000);
+  const uint32_t o = i < n ? off[i] : 0u;
+  const uint32_t base = __builtin_amdgcn_readfirstlane(o);
+  u32x4 v[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) v[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(base + 1024u * c + 16u * lane), 0, 0);
+  char *L = reinterpret_cast<char *>(&lds[w][0]);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) *reinterpret_cast<u32x4 *>(L + swz(1024u * c + 16u * lane)) = v[c];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const uint32_t r = o - base;
+  u32x4 s = {0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) s += *reinterpret_cast<const u32x4 *>(L + swz(r + 16u * c));
+  if (i < n) out[i] = s[0] ^ s[1] ^ s[2] ^ s[3];
+}
+
 // nat64-shaped data movement: 4 lanes per 256-B frame, 4 x 16-B chunks per
 // lane, output chunk c <- input bytes [16c + SHIFT, 16c + SHIFT + 16).
 template <int SHIFT>
@@ -169,6 +211,16 @@ int main(int argc, char **argv) {
   }
   time_it("aos_window64", algo - 2.0 * n, [&](int r) {
     hipLaunchKernelGGL(aos_window, dim3((n + 255) / 256), dim3(256), 0, st, arena[r], off[r], n,
+                       scratch);
+  });
+#define AOSAUX(AUX)                                                                           \
+  time_it("aos_window64_aux" #AUX, algo - 2.0 * n, [&](int r) {                               \
+    hipLaunchKernelGGL(aos_window_aux<AUX>, dim3((n + 255) / 256), dim3(256), 0, st, arena[r], \
+                       off[r], n, scratch);                                                   \
+  });
+  AOSAUX(0) AOSAUX(1) AOSAUX(2) AOSAUX(3)
+  time_it("lds_window64", algo - 2.0 * n, [&](int r) {
+    hipLaunchKernelGGL(lds_window, dim3((n + 255) / 256), dim3(256), 0, st, arena[r], off[r], n,
                        scratch);
   });
   struct {
