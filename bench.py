@@ -117,7 +117,11 @@ def imix_header_bytes_workload(seed):
 
 def cpu_baseline(w, seconds):
     """The C oracle (CPU restatement of the reference path, test infra) on
-    the same batch, one host core, time-bounded sample."""
+    the same batch, time-bounded samples: one host core, then one thread per
+    core on independent shards (capsule's RSS model: one core per RX queue,
+    shared nothing; nat64 keeps one port map per shard)."""
+    import threading
+
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
 
@@ -125,13 +129,14 @@ def cpu_baseline(w, seconds):
     arena, off, ln = w["arena"], w["off"], w["len"]
     n = len(off)
     p = lambda a: a.ctypes.data  # noqa: E731
-    if w["kind"] == "parse":
-        meta = np.zeros(n, np.uint32)
-        csum = np.zeros(n, np.uint32)
-        h = np.zeros(n, np.uint64)
-        run = lambda: L.or_parse_batch(p(arena), p(off), p(ln), n, w["flags"], p(meta),  # noqa
-                                       p(csum), p(h), None)
-    else:
+
+    def make_run():
+        if w["kind"] == "parse":
+            meta = np.zeros(n, np.uint32)
+            csum = np.zeros(n, np.uint32)
+            h = np.zeros(n, np.uint64)
+            return lambda: L.or_parse_batch(p(arena), p(off), p(ln), n, w["flags"], p(meta),
+                                            p(csum), p(h), None)
         pm = oracle_lib.PortMap()
         out = np.zeros(len(arena), np.uint8)
         olen = np.zeros(n, np.uint16)
@@ -141,20 +146,41 @@ def cpu_baseline(w, seconds):
         if w["kind"] == "nat64_4to6":
             pm.nat_6to4(*w["setup"])  # same port map as the device side
             fn = L.or_nat64_4to6
-        run = lambda: fn(pm.h, p(arena), p(off), p(ln), n, p(out), p(off),  # noqa
-                         p(olen), p(disp), p(st))
-    run()  # warm
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        run()
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
+        return lambda: (pm, fn(pm.h, p(arena), p(off), p(ln), n, p(out), p(off),
+                               p(olen), p(disp), p(st)))
+
+    def timed(run, secs):
+        run()  # warm
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            run()
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= secs:
+                return passes, el
+
+    passes, el = timed(make_run(), seconds)
     res = {"value": round(passes * n / el / 1e6, 3), "unit": "Mpps", "cores": 1,
            "kind": "port",
            "sample": f"C oracle (oracle/oracle.c) over the same {n}-packet batch, "
                      f"{passes} passes, {el:.1f} s, 1 thread"}
+    # one shard per core: ctypes drops the GIL for the duration of each call
+    threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
+    runs = [make_run() for _ in range(threads)]
+    got = [None] * threads
+
+    def worker(t):
+        got[t] = timed(runs[t], min(5.0, seconds))
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    res["all_cores"] = {"threads": threads,
+                        "value": round(sum(pp * n / e for pp, e in got) / 1e6, 3),
+                        "sample": f"{threads} threads, each its own shard replica of the "
+                                  f"{n}-packet batch, ~{min(5.0, seconds):.0f} s"}
     if w["kind"] == "parse" and w["frame"] == "64B":
         # the reference bench's own routine (bench/packets.rs:65-69 multi_parse_udp),
         # batches of 500 like bench/packets.rs:31
@@ -183,6 +209,9 @@ def main():
                     choices=["parse64", "imix", "imix_csum", "nat64", "nat64_4to6"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="parse configs: replay the launch cycle as a HIP graph (measured "
+                         "slower than direct launches on MI355X: kept for comparison)")
     ap.add_argument("--e2e", action="store_true",
                     help="host-resident batches: pinned H2D + parse + D2H, pipelined (DESIGN.md §8)")
     args = ap.parse_args()
@@ -239,6 +268,30 @@ def main():
         launch(k)
     torch.cuda.synchronize(dev)
 
+    cycle = 2 * copies
+    if w["kind"] == "parse" and args.graph:
+        # Replay the launch cycle as a HIP graph (launch k still processes
+        # copy k mod R).  On MI355X the graph's node dispatch was measured at
+        # ~1 us per launch slower than direct back-to-back launches.
+        stream = torch.cuda.Stream(dev)
+        glaunch = [packets.ParseLauncher(ctx, batches[k % copies], outs[k & 1], w["flags"], stream)
+                   for k in range(cycle)]
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            for f in glaunch:
+                f()
+        torch.cuda.synchronize(dev)
+
+        whole = args.steps - args.steps % cycle  # timed launches covered by replays
+
+        def launch(k):  # noqa: F811 -- timed launch k (k >= warmup)
+            j = k - args.warmup
+            if j >= whole:
+                glaunch[j % cycle]()  # the remainder, launched directly
+            elif j % cycle == 0:
+                with torch.cuda.stream(stream):
+                    graph.replay()  # launches j .. j + cycle - 1
+
     step = [0]
     # HIP events on the launch stream bracket the K launches of the timed
     # region: their span / K is the average device time per launch (kernel
@@ -285,6 +338,8 @@ def main():
         "data": "synthetic (seeded proptest-style reconciled frames, one shard per rank)",
         "config": {"workload": w["desc"], "config": args.config, "packets_per_step": n,
                    "global_batch": n * g.world, "resident_copies": copies,
+                   "launch": ("hip graph replays of %d launches" % cycle
+                              if w["kind"] == "parse" and args.graph else "direct"),
                    "parallelism": f"{g.world} independent RX-queue shards (no collective)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -12,24 +12,28 @@
 //
 // The reference assigns gateway ports from a global AtomicU16 (first 1025)
 // in first-seen order of (v6 src, tcp src port).  A batch reproduces that
-// order exactly.  Each direction is one fused kernel per 256-frame block:
-//   phase 1  one lane per frame: classify by the reference control flow
-//            (Act / Drop / Abort), look the key up in the device port map
-//            (6to4: open-addressing PORT_MAP; 4to6: the ADDR_MAP reverse
-//            array), and build the frame's new IP header into an LDS record.
-//   phase 2  kFG lanes per frame: stream the frame to its output slot, 16-B
-//            chunks interleaved across the group (chunk c = 16q + kFG*j + g),
-//            each lane loading the input shifted by the header-size change,
-//            the header words patched in registers, the TCP span summed with
-//            v_sad_u16 and reduced across the group; the lane holding the
-//            TCP checksum field stores it last.
+// order exactly.  Each direction is one fused kernel in which a quad of 4
+// lanes owns one frame (16 frames per wave, no LDS, no barrier):
+//   - the quad issues its frame's first 256 output bytes as 16-B loads (lane
+//     g: output chunks 4j + g) together with the header chunks, so the frame
+//     streams in while the header is decoded.  A 16-B-aligned frame is read
+//     with aligned loads and realigned by DPP quad permutes (the 20-byte
+//     header-size change is one chunk + one dword); otherwise each lane loads
+//     at the shifted position;
+//   - DPP quad broadcasts give every lane the header dwords; each lane
+//     classifies by the reference control flow (Act / Drop / Abort);
+//   - lane 0 looks the key up in the device port map (6to4: open-addressing
+//     PORT_MAP; 4to6: the ADDR_MAP reverse array, read by the whole quad);
+//   - each lane patches its chunks in registers and sums its part of the TCP
+//     span with v_sad_u16; the quad reduces; the lane holding the TCP
+//     checksum field stores it last.
 // A 6to4 frame whose key is not yet committed (first seen in this batch)
-// needs the batch-wide first-seen order, so phase 1 defers it: its header
-// record goes to global scratch and its index to a deferred list, and
+// needs the batch-wide first-seen order, so the fused kernel defers it: its
+// header record goes to global scratch and its index to a deferred list, and
 //   K2 count   per-workgroup count of "first packet of a new key"
 //   K3 scan    exclusive scan of the counts (one workgroup) + NEXT_PORT
 //   K4 assign  ballot/popcount prefix -> ordinal -> port = base + ordinal
-//   K5 rewrite the deferred frames (phase 2's code, list-driven) + commit
+//   K5 rewrite the deferred frames (the same quad rewrite, list-driven) + commit
 // finish them.  When no key is new (the steady state) K2..K5 see an empty
 // deferred list and return at once.  Kernel boundaries are the only
 // cross-workgroup hand-offs besides device-scope atomics on the table.
@@ -42,10 +46,11 @@ namespace cgpu {
 namespace {
 
 constexpr uint32_t kBlock = 256;
-#ifndef CGPU_NAT64_FG
-#define CGPU_NAT64_FG 4
+#ifndef CGPU_NAT64_WPE
+#define CGPU_NAT64_WPE 1
 #endif
-constexpr uint32_t kFG = CGPU_NAT64_FG;      // lanes per frame in the rewrite phase
+#define NAT64_OCC __attribute__((amdgpu_waves_per_eu(CGPU_NAT64_WPE)))
+constexpr uint32_t kFG = 4u;                 // lanes per frame in the rewrite phase
 constexpr uint32_t kFJ = 16u / kFG;          // 16-B chunks per lane per 256-B pass
 constexpr uint32_t kNow = 4u;                // record info bit: rewrite in the fused kernel
 constexpr uint32_t kNoSlot = 0xffffffffu;
@@ -98,32 +103,10 @@ struct V6 {
   uint32_t L[11];  // L3-relative dwords: v6 header 0..9, TCP source port in L[10] lo
 };
 
-// Frame-relative dwords 0..19 (80 B) -> V6.  Fast path: dword-aligned frames
-// well inside the arena (wave-uniform), otherwise the tail-safe loader.
-__device__ __forceinline__ void classify(rsrc_t rs, uint32_t arena_len, uint32_t off,
-                                         uint32_t len, V6 &v) {
-  constexpr int NW = 20;
-  uint32_t P[NW];
-  const bool slow = (off & 3u) != 0u || (uint64_t)off + 80u > (uint64_t)arena_len;
-  if (__ballot(slow)) {
-    const uint32_t sh = off & 3u, base = off - sh;
-    const uint32_t need = sh + (len < 80u ? len : 80u);
-    uint32_t D[NW + 1];
-#pragma unroll
-    for (int j = 0; j < NW + 1; ++j)
-      D[j] = (uint32_t)(4 * j) < need ? load4_tail(rs, base + 4u * j, arena_len) : 0u;
-#pragma unroll
-    for (int j = 0; j < NW; ++j) P[j] = __builtin_amdgcn_alignbyte(D[j + 1], D[j], sh);
-  } else {
-#pragma unroll
-    for (int c = 0; c < NW / 4; ++c) {
-      const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u * c), 0, 0);
-      P[4 * c] = q[0];
-      P[4 * c + 1] = q[1];
-      P[4 * c + 2] = q[2];
-      P[4 * c + 3] = q[3];
-    }
-  }
+// V6 from frame-relative dwords P[3..16] (bytes 12..67: the VLAN marker
+// through the TCP source port at QinQ depth); the checks follow the
+// reference nat_6to4 control flow in order.
+__device__ __forceinline__ void classify_dwords(const uint32_t (&P)[20], uint32_t len, V6 &v) {
   const uint32_t marker = be16_lo(P[3]);
   v.k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
   v.eth_len = 14u + 4u * v.k;
@@ -156,6 +139,24 @@ __device__ __forceinline__ void classify(rsrc_t rs, uint32_t arena_len, uint32_t
   if (tcp_off + 20u > new_len) { v.st = CGPU_PKT_L4_OUT_OF_BUFFER; return; }
   v.st = CGPU_PKT_OK;
   v.disp = CGPU_ACT;
+}
+
+// One lane's own classification of a frame (the port-map probe reads a
+// batch-local key's representative frame with it): tail-safe dword loads of
+// bytes 0..79, zero past the frame end.
+__device__ __forceinline__ void classify(rsrc_t rs, uint32_t arena_len, uint32_t off,
+                                         uint32_t len, V6 &v) {
+  constexpr int NW = 20;
+  uint32_t P[NW];
+  const uint32_t sh = off & 3u, base = off - sh;
+  const uint32_t need = sh + (len < 80u ? len : 80u);
+  uint32_t D[NW + 1];
+#pragma unroll
+  for (int j = 0; j < NW + 1; ++j)
+    D[j] = (uint32_t)(4 * j) < need ? load4_tail(rs, base + 4u * j, arena_len) : 0u;
+#pragma unroll
+  for (int j = 0; j < NW; ++j) P[j] = __builtin_amdgcn_alignbyte(D[j + 1], D[j], sh);
+  classify_dwords(P, len, v);
 }
 
 // key = (v6 src, tcp src port) = assigned_port(src, port) (main.rs:129,142-143)
@@ -206,7 +207,7 @@ __device__ __forceinline__ void store_out(rsrc_t ors, uint8_t *out_arena, uint32
   }
 }
 
-// ---- phase 1 of 6to4: classify + probe + IPv4 header -----------------------
+// ---- 6to4: the new IPv4 header, the port-map probe ---------------------------
 // The pushed IPv4 header (v4.rs:594-609) with the setters of main.rs:133-138
 // and Ipv4::reconcile (v4.rs:486-489) already applied, as 5 LE dwords.
 __device__ __forceinline__ void ipv4_header(const V6 &v, uint32_t len, uint32_t (&H)[5]) {
@@ -277,7 +278,7 @@ __device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, rsrc_t rs, ui
   return kNoSlot;
 }
 
-// ---- phase 2 / K5: the rewrite of one frame by its group of kFG lanes --------
+// ---- the rewrite of one frame by its quad (fused kernels and K5) -------------
 // A frame record: info = k | kNow | port << 16 (6to4: the assigned port;
 // 4to6: the original v6-side port); V = the new IP header as LE dwords (6to4:
 // IPv4 H[0..4]; 4to6: the 40-B IPv6 header); ph = 4to6 pseudo-header residue.
@@ -321,33 +322,119 @@ __device__ __forceinline__ void store_chunk(rsrc_t ors, uint8_t *out_arena, uint
     if (b0 < nl) store_out(ors, out_arena, o_off, c, v, nl, (o_off & 3u) == 0u);
     return;
   }
-  __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(b0 + 16u <= nl ? o_off + b0 : kNoRead), 0, 0);
-  if (b0 < nl && b0 + 16u > nl) {  // the partial last chunk: dword and byte stores
-#pragma unroll
-    for (uint32_t t = 0; t < 4u; ++t) {
-      const uint32_t b = b0 + 4u * t;
-      __builtin_amdgcn_raw_buffer_store_b32(v[t], ors, (int)(b + 4u <= nl ? o_off + b : kNoRead), 0, 0);
-#pragma unroll
-      for (uint32_t x = 0; x < 3u; ++x)
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[t] >> (8u * x)), ors,
-                                             (int)(b + 4u > nl && b + x < nl ? o_off + b + x : kNoRead), 0, 0);
+  if (b0 + 16u <= nl) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(o_off + b0), 0, 0);
+  } else if (b0 < nl) {
+    // The partial last chunk, r = 1..15 bytes: its whole dwords in one
+    // b32/b64/b96 store, then a b16 and/or b8 for the trailing bytes.  With
+    // a wave-uniform frame length only one of the paths below is issued.
+    const uint32_t r = nl - b0, d = r >> 2, tb = r & 3u, o = o_off + b0;
+    if (d == 3u) {
+      __builtin_amdgcn_raw_buffer_store_b96(u32x3{v[0], v[1], v[2]}, ors, (int)o, 0, 0);
+    } else if (d == 2u) {
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{v[0], v[1]}, ors, (int)o, 0, 0);
+    } else if (d == 1u) {
+      __builtin_amdgcn_raw_buffer_store_b32(v[0], ors, (int)o, 0, 0);
+    }
+    if (tb != 0u) {
+      const uint32_t w = d == 0u ? v[0] : (d == 1u ? v[1] : (d == 2u ? v[2] : v[3]));
+      const uint32_t ob = o + 4u * d;
+      if (tb >= 2u) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)w, ors, (int)ob, 0, 0);
+      if (tb & 1u) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> (8u * (tb & 2u))), ors,
+                                                       (int)(ob + (tb & 2u)), 0, 0);
     }
   }
 }
 
 // Output byte b of the rewritten frame comes from input byte b (Ethernet,
 // chunks 0-1), from the header record, or from input byte b + 20 (6to4) /
-// b - 20 (4to6) (the TCP segment, chunks >= 2).  FAST (wave-uniform): every
-// frame of the wave is dword-aligned on both sides and well inside both
-// arenas, so loads and full-chunk stores are branch-free (an unneeded chunk
-// gets an offset past num_records: zero load, dropped store).
+// b - 20 (4to6) (the TCP segment, chunks >= 2).  A group of kFG = 16 lanes
+// owns a frame; lane g owns output chunks c = 16q + g.
+constexpr uint32_t kHdrC4 = 4u, kHdrC6 = 5u;  // chunks holding header words / patches
+constexpr uint32_t kHold4 = 3u, kHold6 = 4u;  // chunk holding the TCP checksum field
+
+// Output chunk c of frame f, its 16 bytes o as taken from the input: patch
+// the header dwords, add the TCP span bytes to acc, store it (or keep it in
+// `held` if it carries the checksum field).
 template <bool TO4, bool FAST>
-__device__ __forceinline__ void rewrite_frame(const Nat64Args &a, rsrc_t rs, rsrc_t ors, uint32_t g,
-                                              const FrameRec &f, bool in_al_wave) {
-  constexpr uint32_t kHdrC = TO4 ? 4u : 5u;  // chunks holding header words / patches
-  constexpr uint32_t kHold = TO4 ? 3u : 4u;  // chunk holding the TCP checksum field
-  constexpr int kSpanR = TO4 ? 8 : 13;       // first TCP dword (its high half)
+__device__ __forceinline__ void chunk_out(const Nat64Args &a, rsrc_t ors, const FrameRec &f,
+                                          uint32_t c, u32x4 o, uint32_t &acc, u32x4 &held) {
+  constexpr uint32_t kHdrC = TO4 ? kHdrC4 : kHdrC6;
+  constexpr uint32_t kHold = TO4 ? kHold4 : kHold6;
+  constexpr int kSpanR = TO4 ? 8 : 13;  // first TCP dword (its high half)
   const uint32_t k = f.info & 3u, port_be = swap16(f.info >> 16), nl = f.new_len;
+  if (16u * c >= nl) return;
+  if (c < kHdrC) {
+#pragma unroll
+    for (uint32_t t = 0; t < 4u; ++t) {
+      const int r = (int)(4u * c + t) - (int)k;
+      const uint32_t d = out_dword<TO4>(r, o[t], f.V, port_be);
+      uint32_t m = r < kSpanR ? 0u : (r == kSpanR ? 0xffff0000u : 0xffffffffu);
+      m &= range_mask(16u * c + 4u * t, 0u, nl);
+      acc = sad16(d & m, acc);
+      o[t] = d;
+    }
+  } else {
+    acc = sad16(o[3], sad16(o[2], sad16(o[1], sad16(o[0], acc))));
+    if (16u * c + 16u > nl) {  // bytes past the end of the frame
+#pragma unroll
+      for (uint32_t t = 0; t < 4u; ++t) {
+        const uint32_t x = o[t] & ~range_mask(16u * c + 4u * t, 0u, nl);
+        acc -= (x & 0xffffu) + (x >> 16);
+      }
+    }
+  }
+  if (c == kHold) held = o;
+  else store_chunk<FAST>(ors, a.out_arena, f.o_off, c, o, nl);
+}
+
+// The group's TCP sum, the checksum (v4 or v6 pseudo-header) into the held
+// chunk, and its store by the lane that owns it.
+template <bool TO4, bool FAST>
+__device__ __forceinline__ void finish_frame(const Nat64Args &a, rsrc_t ors, const FrameRec &f,
+                                             uint32_t g, uint32_t acc, u32x4 held) {
+  constexpr uint32_t kHold = TO4 ? kHold4 : kHold6;
+  const uint32_t k = f.info & 3u, nl = f.new_len;
+#pragma unroll
+  for (uint32_t d = kFG / 2; d > 0; d >>= 1) acc += __shfl_xor(acc, d, kFG);
+  if (g != kHold % kFG) return;
+  uint32_t tcp_c;
+  if (TO4) {
+    // v4 pseudo-header (checksum.rs:93-103): 203.0.113.1, dst, 6, span
+    const uint32_t span = (nl - (34u + 4u * k)) & 0xffffu;
+    const uint32_t dst = be32(f.V[4]);
+    const uint32_t ph = fold32(0xcb00u + 0x7101u + (dst >> 16) + (dst & 0xffffu) + 6u + span);
+    tcp_c = (~fold32(ph + swap16(fold32(acc)))) & 0xffffu;
+  } else {
+    // v6 pseudo-header (checksum.rs:123-128): addresses (ph), span, 6
+    const uint32_t span = (nl - (54u + 4u * k)) & 0xffffu;
+    tcp_c = (~fold32(swap16(fold32(acc + f.ph)) + span + 6u)) & 0xffffu;
+  }
+  const uint32_t tw = TO4 ? k : k + 1u;  // dword of the checksum field in the held chunk
+#pragma unroll
+  for (uint32_t t = 0; t < 4u; ++t)
+    if (t == tw) held[t] |= swap16(tcp_c) << 16;
+  store_chunk<FAST>(ors, a.out_arena, f.o_off, kHold, held, nl);
+}
+
+// Input position of output chunk c (16 input bytes at the shifted position).
+template <bool TO4>
+__device__ __forceinline__ uint32_t chunk_src(uint32_t in_off, uint32_t c) {
+  return c < 2u ? in_off + 16u * c : (TO4 ? in_off + 16u * c + 20u : in_off + 16u * c - 20u);
+}
+
+// A group of kFG lanes rewrites frame f; lane g owns output chunks
+// c = 16q + kFG j + g (interleaved: each load instruction covers whole 64-B
+// pieces of kBlock / kFG frames).  FAST (wave-uniform): every frame of the
+// wave is dword-aligned on both sides and well inside both arenas, so loads
+// and full-chunk stores are branch-free (an unneeded chunk gets an offset
+// past num_records: zero load, dropped store).  PRE: the pass-0 chunks were
+// loaded by the caller (FAST only).
+template <bool TO4, bool FAST, bool PRE>
+__device__ __forceinline__ void rewrite_frame(const Nat64Args &a, rsrc_t rs, rsrc_t ors, uint32_t g,
+                                              const FrameRec &f, bool in_al_wave,
+                                              const u32x4 (&pre)[kFJ]) {
+  const uint32_t nl = f.new_len;
   uint32_t acc = 0;
   u32x4 held = {0u, 0u, 0u, 0u};
   for (uint32_t q = 0; 256u * q < nl; ++q) {
@@ -355,156 +442,287 @@ __device__ __forceinline__ void rewrite_frame(const Nat64Args &a, rsrc_t rs, rsr
 #pragma unroll
     for (uint32_t j = 0; j < kFJ; ++j) {
       const uint32_t c = 16u * q + kFG * j + g;
-      const uint32_t src = c < 2u ? f.in_off + 16u * c
-                                  : (TO4 ? f.in_off + 16u * c + 20u : f.in_off + 16u * c - 20u);
       const bool need = 16u * c < nl;
-      if (FAST) {
-        o[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(need ? src : kNoRead), 0, 0);
+      if (PRE && q == 0u) {
+        o[j] = pre[j];
+      } else if (FAST) {
+        o[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(need ? chunk_src<TO4>(f.in_off, c) : kNoRead), 0, 0);
       } else {
         o[j] = u32x4{0u, 0u, 0u, 0u};
-        if (need) o[j] = load_in(rs, a.arena_len, src, in_al_wave);
+        if (need) o[j] = load_in(rs, a.arena_len, chunk_src<TO4>(f.in_off, c), in_al_wave);
       }
     }
 #pragma unroll
-    for (uint32_t j = 0; j < kFJ; ++j) {
-      const uint32_t c = 16u * q + kFG * j + g;
-      if (c < kHdrC) {
-#pragma unroll
-        for (uint32_t t = 0; t < 4u; ++t) {
-          const int r = (int)(4u * c + t) - (int)k;
-          const uint32_t d = out_dword<TO4>(r, o[j][t], f.V, port_be);
-          uint32_t m = r < kSpanR ? 0u : (r == kSpanR ? 0xffff0000u : 0xffffffffu);
-          m &= range_mask(16u * c + 4u * t, 0u, nl);
-          acc = sad16(d & m, acc);
-          o[j][t] = d;
-        }
-      } else {
-        acc = sad16(o[j][3], sad16(o[j][2], sad16(o[j][1], sad16(o[j][0], acc))));
-        if (16u * c < nl && 16u * c + 16u > nl) {  // bytes past the end of the frame
-#pragma unroll
-          for (uint32_t t = 0; t < 4u; ++t) {
-            const uint32_t x = o[j][t] & ~range_mask(16u * c + 4u * t, 0u, nl);
-            acc -= (x & 0xffffu) + (x >> 16);
-          }
-        }
-      }
-      if (c == kHold) held = o[j];
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < kFJ; ++j) {
-      const uint32_t c = 16u * q + kFG * j + g;
-      if (c != kHold) store_chunk<FAST>(ors, a.out_arena, f.o_off, c, o[j], nl);
-    }
+    for (uint32_t j = 0; j < kFJ; ++j) chunk_out<TO4, FAST>(a, ors, f, 16u * q + kFG * j + g, o[j], acc, held);
   }
-#pragma unroll
-  for (uint32_t d = kFG / 2; d > 0; d >>= 1) acc += __shfl_xor(acc, d, kFG);
-  if (g == kHold % kFG) {
-    uint32_t tcp_c;
-    if (TO4) {
-      // v4 pseudo-header (checksum.rs:93-103): 203.0.113.1, dst, 6, span
-      const uint32_t span = (nl - (34u + 4u * k)) & 0xffffu;
-      const uint32_t dst = be32(f.V[4]);
-      const uint32_t ph = fold32(0xcb00u + 0x7101u + (dst >> 16) + (dst & 0xffffu) + 6u + span);
-      tcp_c = (~fold32(ph + swap16(fold32(acc)))) & 0xffffu;
-    } else {
-      // v6 pseudo-header (checksum.rs:123-128): addresses (ph), span, 6
-      const uint32_t span = (nl - (54u + 4u * k)) & 0xffffu;
-      tcp_c = (~fold32(swap16(fold32(acc + f.ph)) + span + 6u)) & 0xffffu;
-    }
-    const uint32_t tw = TO4 ? k : k + 1u;  // dword of the checksum field in the held chunk
-#pragma unroll
-    for (uint32_t t = 0; t < 4u; ++t)
-      if (t == tw) held[t] |= swap16(tcp_c) << 16;
-    store_chunk<FAST>(ors, a.out_arena, f.o_off, kHold, held, nl);
-  }
+  finish_frame<TO4, FAST>(a, ors, f, g, acc, held);
 }
 
-// Runs rewrite_frame with the wave-uniform FAST decision.
+// Runs rewrite_frame with the wave-uniform FAST decision (K5's frames).
+template <bool TO4>
+__device__ __forceinline__ bool wave_fast(const Nat64Args &a, bool act, const FrameRec &f) {
+  return !__ballot(act && !((f.in_off & 3u) == 0u && (f.o_off & 3u) == 0u &&
+                            (uint64_t)f.in_off + f.new_len + 64u <= (uint64_t)a.arena_len &&
+                            (uint64_t)f.o_off + f.new_len + 16u <= (uint64_t)a.out_arena_len));
+}
+
 template <bool TO4>
 __device__ __forceinline__ void rewrite_dispatch(const Nat64Args &a, rsrc_t rs, rsrc_t ors,
-                                                 uint32_t g, const FrameRec &f) {
-  const bool fast = !__ballot(!((f.in_off & 3u) == 0u && (f.o_off & 3u) == 0u &&
-                                (uint64_t)f.in_off + f.new_len + 64u <= (uint64_t)a.arena_len &&
-                                (uint64_t)f.o_off + f.new_len + 16u <= (uint64_t)a.out_arena_len));
-  if (fast) {
-    rewrite_frame<TO4, true>(a, rs, ors, g, f, true);
+                                                 uint32_t g, const FrameRec &f, bool act) {
+  const u32x4 none[kFJ] = {};
+  if (wave_fast<TO4>(a, act, f)) {
+    if (act) rewrite_frame<TO4, true, false>(a, rs, ors, g, f, true, none);
   } else {
-    const bool in_al_wave = !__ballot((f.in_off & 3u) != 0u);
-    rewrite_frame<TO4, false>(a, rs, ors, g, f, in_al_wave);
+    const bool in_al_wave = !__ballot(act && (f.in_off & 3u) != 0u);
+    if (act) rewrite_frame<TO4, false, false>(a, rs, ors, g, f, in_al_wave, none);
   }
 }
 
-// Phase 2 of the fused kernels: the block's ready frames, kBlock / kFG at a
-// time.  LDS record (4 x 16 B): {in_off, o_off, new_len, info}, V[0..3],
-// V[4..7], {V[8], V[9], ph, -}.
+// ---- fused kernels: one 4-lane quad per frame -----------------------------
+// Lane g of the quad owns output chunks c = 16q + 4j + g.  The quad issues
+// its frame's pass-0 loads (4 x 16 B per lane, at the shifted input
+// positions) together with the header chunks 0..3 (and lane 0: chunk 4),
+// unshifted, which hit the same lines; the header dwords reach every lane of
+// the quad by DPP quad broadcasts; every lane classifies (the work is 4x
+// redundant, but no LDS, no barrier, and a frame's bytes are read while its
+// lines are hot); lane 0 probes the port map; then the quad rewrites.
+
+// Lane K of each quad, to all four lanes (DPP quad_perm [K, K, K, K]).
+template <int K>
+__device__ __forceinline__ uint32_t qbc(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xf, 0xf, true);
+}
+
+// Header chunk g (lanes 0..3) and, in lane 0, chunk 4: frame bytes 0..79.
+__device__ __forceinline__ void header_loads(rsrc_t rs, uint32_t arena_len, uint32_t off, uint32_t g,
+                                             bool valid, bool hdr_fast, bool al_wave, u32x4 &Y,
+                                             u32x4 &Y4) {
+  Y = u32x4{0u, 0u, 0u, 0u};
+  Y4 = u32x4{0u, 0u, 0u, 0u};
+  if (hdr_fast) {
+    Y = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(valid ? off + 16u * g : kNoRead), 0, 0);
+    Y4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(valid && g == 0u ? off + 64u : kNoRead), 0, 0);
+  } else if (valid) {
+    Y = load_in(rs, arena_len, off + 16u * g, al_wave);
+    if (g == 0u) Y4 = load_in(rs, arena_len, off + 64u, al_wave);
+  }
+}
+
+// Frame dwords P[3..16] (bytes 12..67) in every lane of the quad.
+__device__ __forceinline__ void gather_header(u32x4 Y, u32x4 Y4, uint32_t (&P)[20]) {
+#pragma unroll
+  for (int j = 0; j < 20; ++j) P[j] = 0u;
+  P[3] = qbc<0>(Y[3]);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    P[4 + t] = qbc<1>(Y[t]);
+    P[8 + t] = qbc<2>(Y[t]);
+    P[12 + t] = qbc<3>(Y[t]);
+  }
+  P[16] = qbc<0>(Y4[0]);
+}
+
+// Pass-0 chunk loads of the quad's frame (FAST only; zero otherwise).
 template <bool TO4>
-__device__ __forceinline__ void rewrite_block(const Nat64Args &a, const u32x4 (*lrec)[4]) {
-  const uint32_t g = threadIdx.x % kFG;
+__device__ __forceinline__ void pass0_loads(rsrc_t rs, uint32_t off, uint32_t nl, uint32_t g, bool fast,
+                                            u32x4 (&X)[kFJ]) {
+#pragma unroll
+  for (uint32_t j = 0; j < kFJ; ++j) {
+    const uint32_t c = kFG * j + g;
+    X[j] = u32x4{0u, 0u, 0u, 0u};
+    if (fast) X[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * c < nl ? chunk_src<TO4>(off, c) : kNoRead), 0, 0);
+  }
+}
+
+// One quad's frame descriptor for a round and the wave-uniform load modes.
+struct QuadDesc {
+  uint32_t i, off, len, o_off, nl;
+  bool valid, fast, hdr_fast, al_wave;
+};
+
+// TO4: 6to4 (an Act frame has 74 <= len, new length len - 20); else 4to6
+// (54 <= len < 2028, new length len + 20).
+template <bool TO4>
+__device__ __forceinline__ QuadDesc quad_desc(const Nat64Args &a, uint32_t i) {
+  QuadDesc d;
+  d.i = i;
+  d.valid = i < a.n;
+  d.off = d.valid ? a.off[i] : 0u;
+  d.len = d.valid ? (uint32_t)a.len[i] : 0u;
+  d.o_off = d.valid ? a.out_off[i] : 0u;
+  return d;
+}
+
+template <bool TO4>
+__device__ __forceinline__ void quad_modes(const Nat64Args &a, QuadDesc &d) {
+  const bool cand = TO4 ? (d.valid && d.len >= 74u) : (d.valid && d.len >= 54u && d.len < kDataRoom - 20u);
+  d.nl = cand ? (TO4 ? d.len - 20u : d.len + 20u) : 0u;
+  d.fast = !__ballot(cand && !((d.off & 3u) == 0u && (d.o_off & 3u) == 0u &&
+                               (uint64_t)d.off + d.nl + 64u <= (uint64_t)a.arena_len &&
+                               (uint64_t)d.o_off + d.nl + 16u <= (uint64_t)a.out_arena_len));
+  d.hdr_fast = !__ballot(d.valid && ((d.off & 3u) != 0u || (uint64_t)d.off + 80u > (uint64_t)a.arena_len));
+  d.al_wave = !__ballot(d.valid && (d.off & 3u) != 0u);
+}
+
+// ---- realignment within the quad ---------------------------------------------
+// 20 bytes = one chunk + one dword, so when the input frame is 16-B aligned
+// every output chunk c >= 2 is three dwords of one aligned input chunk and
+// one dword of its neighbour, which another lane of the quad loaded:
+//   6to4: out c = {in(c+1).y, .z, .w, in(c+2).x}: lane g loads in(c+1) and
+//         takes in(c+2).x from lane g+1 (lane 3: from lane 0's next chunk);
+//   4to6: out c = {in(c-2).w, in(c-1).x, .y, .z}: lane g loads in(c-1) and
+//         takes in(c-2).w from lane g-1 (lane 0: lane 3's previous chunk).
+// Chunks 0 and 1 are the input's own.  Aligned loads cost one 16-B piece of
+// one line each; the shifted ones straddled two (measured 134 vs 92 us for
+// the bare copy of 1 M 256-B frames).
+template <int CTRL>
+__device__ __forceinline__ uint32_t qdpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
+}
+constexpr int kQNext = 1 | (2 << 2) | (3 << 4) | (0 << 6);  // lane g <- lane (g + 1) % 4
+constexpr int kQPrev = 3 | (0 << 2) | (1 << 4) | (2 << 6);  // lane g <- lane (g + 3) % 4
+
+template <bool TO4>
+__device__ __forceinline__ uint32_t aligned_src(uint32_t in_off, uint32_t c) {
+  if (c < 2u) return in_off + 16u * c;
+  return TO4 ? in_off + 16u * (c + 1u) : in_off + 16u * (c - 1u);
+}
+
+// Pass q's aligned loads A[j] (chunk c = 16q + 4j + g) and, 6to4, lane 3's
+// extra dword E = in(16q + 17).x for output chunk 16q + 15.
+template <bool TO4>
+__device__ __forceinline__ void aligned_loads(rsrc_t rs, uint32_t in_off, uint32_t nl, uint32_t q,
+                                              uint32_t g, u32x4 (&A)[kFJ], uint32_t &E) {
+#pragma unroll
+  for (uint32_t j = 0; j < kFJ; ++j) {
+    const uint32_t c = 16u * q + kFG * j + g;
+    // 6to4: chunk c's load also serves output chunk c - 1's last dword
+    const bool need = TO4 ? 16u * c < nl + 4u : 16u * c < nl;
+    A[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(need ? aligned_src<TO4>(in_off, c) : kNoRead), 0, 0);
+  }
+  E = 0u;
+  if (TO4) {
+    const uint32_t c = 16u * q + 15u;
+    E = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(g == 3u && 16u * c < nl ? in_off + 16u * (c + 2u) : kNoRead), 0, 0);
+  }
+}
+
+// The shifted chunks X[j] of pass q from the aligned loads.  carry (4to6):
+// lane 3's A[3].w of the previous pass, as seen by lane 0.
+template <bool TO4>
+__device__ __forceinline__ void realign(const u32x4 (&A)[kFJ], uint32_t E, uint32_t q, uint32_t g,
+                                        uint32_t &carry, u32x4 (&X)[kFJ]) {
+#pragma unroll
+  for (uint32_t j = 0; j < kFJ; ++j) {
+    if (TO4) {
+      const uint32_t n1 = qdpp<kQNext>(A[j][0]);
+      const uint32_t n2 = j + 1 < kFJ ? qdpp<kQNext>(A[j + 1 < kFJ ? j + 1 : j][0]) : E;
+      const uint32_t nx = g == 3u ? n2 : n1;
+      X[j] = (q == 0u && j == 0u && g < 2u) ? A[j] : u32x4{A[j][1], A[j][2], A[j][3], nx};
+    } else {
+      const uint32_t p1 = qdpp<kQPrev>(A[j][3]);
+      const uint32_t p0 = j > 0 ? qdpp<kQPrev>(A[j > 0 ? j - 1 : 0][3]) : carry;
+      uint32_t pw = g == 0u ? p0 : p1;
+      if (q == 0u && j == 0u) {
+        const uint32_t c0w = qbc<0>(A[0][3]);  // in(0).w for output chunk 2
+        if (g == 2u) pw = c0w;
+      }
+      X[j] = (q == 0u && j == 0u && g < 2u) ? A[j] : u32x4{pw, A[j][0], A[j][1], A[j][2]};
+    }
+  }
+  if (!TO4) carry = qdpp<kQPrev>(A[kFJ - 1][3]);  // lane 0 <- lane 3's last chunk
+}
+
+// rewrite_frame for a 16-B-aligned input frame: aligned loads + realign.
+// Pass 0's loads were issued by the caller (A0, E0).
+template <bool TO4>
+__device__ __forceinline__ void rewrite_frame_al(const Nat64Args &a, rsrc_t rs, rsrc_t ors, uint32_t g,
+                                                 const FrameRec &f, const u32x4 (&A0)[kFJ], uint32_t E0) {
+  const uint32_t nl = f.new_len;
+  uint32_t acc = 0, carry = 0;
+  u32x4 held = {0u, 0u, 0u, 0u};
+  u32x4 X[kFJ];
+  realign<TO4>(A0, E0, 0u, g, carry, X);
+#pragma unroll
+  for (uint32_t j = 0; j < kFJ; ++j) chunk_out<TO4, true>(a, ors, f, kFG * j + g, X[j], acc, held);
+  for (uint32_t q = 1; 256u * q < nl; ++q) {  // frames longer than 256 B
+    u32x4 A[kFJ];
+    uint32_t E;
+    aligned_loads<TO4>(rs, f.in_off, nl, q, g, A, E);
+    realign<TO4>(A, E, q, g, carry, X);
+#pragma unroll
+    for (uint32_t j = 0; j < kFJ; ++j) chunk_out<TO4, true>(a, ors, f, 16u * q + kFG * j + g, X[j], acc, held);
+  }
+  finish_frame<TO4, true>(a, ors, f, g, acc, held);
+}
+
+// The quad's frame: aligned (16-B input, FAST), FAST (shifted loads issued
+// early) or general; the pass-0 loads go out with the header loads.
+template <bool TO4>
+__device__ __forceinline__ void issue_frame_loads(rsrc_t rs, const QuadDesc &d, uint32_t g, bool al16,
+                                                  u32x4 (&X)[kFJ], uint32_t &E) {
+  E = 0u;
+  if (al16) aligned_loads<TO4>(rs, d.off, d.nl, 0u, g, X, E);
+  else pass0_loads<TO4>(rs, d.off, d.nl, g, d.fast, X);
+}
+
+template <bool TO4>
+__device__ __forceinline__ void rewrite_quad(const Nat64Args &a, rsrc_t rs, rsrc_t ors, uint32_t g,
+                                             const QuadDesc &d, bool al16, const FrameRec &f,
+                                             const u32x4 (&X)[kFJ], uint32_t E) {
+  if (al16) rewrite_frame_al<TO4>(a, rs, ors, g, f, X, E);
+  else if (d.fast) rewrite_frame<TO4, true, true>(a, rs, ors, g, f, true, X);
+  else rewrite_frame<TO4, false, false>(a, rs, ors, g, f, d.al_wave, X);
+}
+
+__global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a) {
+  const uint32_t lane = threadIdx.x & 63u, g = threadIdx.x & (kFG - 1u);
   const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
   const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
-  for (uint32_t it = 0; it < kFG; ++it) {
-    const uint32_t fl = it * (kBlock / kFG) + threadIdx.x / kFG;
-    const u32x4 r0 = lrec[fl][0];
-    if (!(r0[3] & kNow)) continue;  // uniform within the group
-    const u32x4 r1 = lrec[fl][1], r2 = lrec[fl][2], r3 = lrec[fl][3];
-    FrameRec f;
-    f.in_off = r0[0];
-    f.o_off = r0[1];
-    f.new_len = r0[2];
-    f.info = r0[3];
-    f.V[0] = r1[0]; f.V[1] = r1[1]; f.V[2] = r1[2]; f.V[3] = r1[3];
-    f.V[4] = r2[0]; f.V[5] = r2[1]; f.V[6] = r2[2]; f.V[7] = r2[3];
-    f.V[8] = r3[0]; f.V[9] = r3[1];
-    f.ph = r3[2];
-    rewrite_dispatch<TO4>(a, rs, ors, g, f);
-    if (g == 0u) a.out_len[blockIdx.x * kBlock + fl] = (uint16_t)f.new_len;
-  }
-}
-
-// ---- 6to4 fused kernel ------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void nat64_6to4_fused(Nat64Args a) {
-  __shared__ u32x4 lrec[kBlock][4];
-  const uint32_t t = threadIdx.x, lane = t & 63u;
-  const uint32_t i = blockIdx.x * kBlock + t;
-  const bool valid = i < a.n;
-  const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
-  const uint32_t off = valid ? a.off[i] : 0u, len = valid ? (uint32_t)a.len[i] : 0u;
+  QuadDesc d = quad_desc<true>(a, blockIdx.x * (kBlock / kFG) + threadIdx.x / kFG);
+  quad_modes<true>(a, d);
+  const bool al16 = d.fast && !__ballot(d.nl != 0u && (d.off & 15u) != 0u);
+  u32x4 X[kFJ], Y, Y4;
+  uint32_t E;
+  issue_frame_loads<true>(rs, d, g, al16, X, E);
+  header_loads(rs, a.arena_len, d.off, g, d.valid, d.hdr_fast, d.al_wave, Y, Y4);
+  uint32_t P[20];
+  gather_header(Y, Y4, P);
   V6 v;
-  classify(rs, a.arena_len, off, len, v);
-  bool deferred = false;
-  uint32_t info = 0u;
-  if (valid) {
-    uint32_t slot = kNoSlot;
-    if (v.disp == CGPU_ACT) {
-      uint32_t port;
-      slot = probe_port(a, rs, i, v, port);
-      if (slot == kNoSlot) {
-        v.disp = CGPU_ABORT;
-        v.st = CGPU_PKT_TABLE_FULL;
-      } else {
-        uint32_t H[5];
-        ipv4_header(v, len, H);
-        if (port != 0xffffffffu) {  // committed key: finished in phase 2
-          info = v.k | kNow | (port << 16);
-          lrec[t][0] = u32x4{off, a.out_off[i], len - 20u, info};
-          lrec[t][1] = u32x4{H[0], H[1], H[2], H[3]};
-          lrec[t][2] = u32x4{H[4], 0u, 0u, 0u};
-          slot = kNoSlot;
-        } else {  // new key: its port needs the batch-wide order (K2..K5)
-          deferred = true;
-          a.rec_h[i] = u32x4{H[0], H[1], H[2], H[3]};
-          a.rec_b[i] = make_uint2(H[4], v.k);
-        }
-      }
-    }
-    if (v.disp != CGPU_ACT) a.out_len[i] = 0;
-    a.pkt_slot[i] = slot;
-    a.disposition[i] = (uint8_t)v.disp;
-    a.status[i] = (uint8_t)v.st;
+  classify_dwords(P, d.len, v);
+  // assigned_port (main.rs:41-53): lane 0 of the quad probes the table
+  uint32_t slot = kNoSlot, port = 0xffffffffu;
+  if (d.valid && g == 0u && v.disp == CGPU_ACT) {
+#ifdef CGPU_NAT64_ABL_NOPROBE  // timing ablation only: every key committed, no table access
+    slot = 0u;
+    port = 1025u;
+#else
+    slot = probe_port(a, rs, d.i, v, port);
+#endif
   }
-  if (!(info & kNow)) lrec[t][0] = u32x4{0u, 0u, 0u, 0u};
+  slot = qbc<0>(slot);
+  port = qbc<0>(port);
+  if (v.disp == CGPU_ACT && slot == kNoSlot) {
+    v.disp = CGPU_ABORT;
+    v.st = CGPU_PKT_TABLE_FULL;
+  }
+  const bool act = d.valid && v.disp == CGPU_ACT;
+  uint32_t H[5];
+  ipv4_header(v, d.len, H);
+  const bool now = act && port != 0xffffffffu;  // committed key: finished here
+  const bool deferred = act && !now;            // new key: its port needs the batch order (K2..K5)
+  if (d.valid && g == 0u) {
+    if (deferred) {
+      a.rec_h[d.i] = u32x4{H[0], H[1], H[2], H[3]};
+      a.rec_b[d.i] = make_uint2(H[4], v.k);
+    }
+    a.out_len[d.i] = now ? (uint16_t)d.nl : 0;
+    a.pkt_slot[d.i] = now ? kNoSlot : slot;
+    a.disposition[d.i] = (uint8_t)v.disp;
+    a.status[d.i] = (uint8_t)v.st;
+  }
   // append the deferred frames to the list (one atomic per wave)
-  const uint64_t dm = __ballot(deferred);
+  const uint64_t dm = __ballot(deferred && g == 0u);
   if (dm) {
     const uint32_t leader = (uint32_t)__builtin_ctzll(dm);
     uint32_t base = 0;
@@ -512,10 +730,23 @@ __global__ __launch_bounds__(kBlock) void nat64_6to4_fused(Nat64Args a) {
     base = __shfl(base, (int)leader);
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32),
                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
-    if (deferred) a.defer[base + rank] = i;
+    if (deferred && g == 0u) a.defer[base + rank] = d.i;
   }
-  __syncthreads();
-  rewrite_block<true>(a, lrec);
+#ifndef CGPU_NAT64_ABL_NOREWRITE  // timing ablation only: classify + probe alone
+  if (now) {
+    FrameRec f;
+    f.in_off = d.off;
+    f.o_off = d.o_off;
+    f.new_len = d.nl;
+    f.info = v.k | kNow | (port << 16);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) f.V[j] = H[j];
+#pragma unroll
+    for (int j = 5; j < 10; ++j) f.V[j] = 0u;
+    f.ph = 0u;
+    rewrite_quad<true>(a, rs, ors, g, d, al16, f, X, E);
+  }
+#endif
 }
 
 // Only packets whose key was first seen in this batch touch the table here.
@@ -606,7 +837,7 @@ __global__ __launch_bounds__(kBlock) void nat64_assign(Nat64Args a) {
 
 
 // ---- K5: the deferred frames (phase 2's rewrite, list-driven) + commit -------
-__global__ __launch_bounds__(kBlock) void nat64_6to4_deferred(Nat64Args a) {
+__global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_deferred(Nat64Args a) {
   const uint32_t cnt = a.pm.state[4u + a.par];
   const uint32_t g = threadIdx.x % kFG;
   const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
@@ -626,7 +857,7 @@ __global__ __launch_bounds__(kBlock) void nat64_6to4_deferred(Nat64Args a) {
 #pragma unroll
     for (int j = 5; j < 10; ++j) f.V[j] = 0u;
     f.ph = 0u;
-    rewrite_dispatch<true>(a, rs, ors, g, f);
+    rewrite_dispatch<true>(a, rs, ors, g, f, true);
     if (g == 0u) {
       a.out_len[p] = (uint16_t)f.new_len;
       if (ps & kFirstBit) {  // commit the new key (PORT_MAP.insert_new, main.rs:49)
@@ -640,110 +871,117 @@ __global__ __launch_bounds__(kBlock) void nat64_6to4_deferred(Nat64Args a) {
 }
 
 // ============================ 4to6 direction =================================
-// Phase 1: classify, look the TCP destination port up in the reverse map
-// ADDR_MAP (rev[port] -> slot -> the v6 key), build the IPv6 header; phase 2
-// as in 6to4 with the input shifted by -20 bytes behind the 40-byte header
-// (the TCP checksum field, output bytes 70+4k, is in chunk 4).
-__global__ __launch_bounds__(kBlock) void nat64_4to6_fused(Nat64Args a) {
-  __shared__ u32x4 lrec[kBlock][4];
-  const uint32_t t = threadIdx.x;
-  const uint32_t i = blockIdx.x * kBlock + t;
-  const bool valid = i < a.n;
-  const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
-  const uint32_t off = valid ? a.off[i] : 0u, len = valid ? (uint32_t)a.len[i] : 0u;
-  // frame-relative dwords 0..11 (48 B): Ethernet + IPv4 + TCP ports, QinQ included
-  constexpr int NW = 12;
-  uint32_t P[NW];
-  const bool slow = (off & 3u) != 0u || (uint64_t)off + 48u > (uint64_t)a.arena_len;
-  if (__ballot(slow)) {
-    const uint32_t sh = off & 3u, base = off - sh;
-    const uint32_t need = sh + (len < 48u ? len : 48u);
-    uint32_t D[NW + 1];
+// Classify, look the TCP destination port up in the reverse map ADDR_MAP
+// (rev[port] -> slot -> the v6 key), build the IPv6 header, then the quad
+// rewrite with the input shifted by -20 bytes behind the 40-byte header (the
+// TCP checksum field, output bytes 70+4k, is in chunk 4).
+// 4to6 classification of one frame (main.rs:86-118) up to the ADDR_MAP
+// lookup: disposition, status, VLAN depth, the TCP destination port, and
+// the L3-relative dwords L[0..5].
+struct V4 {
+  uint32_t k, eth_len, disp, st, gw_port;
+  uint32_t L[6];
+};
+
+__device__ __forceinline__ void classify4(const uint32_t (&P)[20], uint32_t len, V4 &v) {
+  const uint32_t marker = be16_lo(P[3]);
+  v.k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
+  v.eth_len = 14u + 4u * v.k;
+  const uint32_t et = be16_lo(sel3(v.k, P[3], P[4], P[5]));
+  uint32_t A[8];  // L3-relative dwords 0..6 (IPv4 header, TCP ports)
 #pragma unroll
-    for (int j = 0; j < NW + 1; ++j)
-      D[j] = (uint32_t)(4 * j) < need ? load4_tail(rs, base + 4u * j, a.arena_len) : 0u;
+  for (int j = 0; j < 8; ++j) A[j] = __builtin_amdgcn_alignbyte(P[4 + j], P[3 + j], 2);
 #pragma unroll
-    for (int j = 0; j < NW; ++j) P[j] = __builtin_amdgcn_alignbyte(D[j + 1], D[j], sh);
-  } else {
-#pragma unroll
-    for (int c = 0; c < NW / 4; ++c) {
-      const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u * c), 0, 0);
-      P[4 * c] = q[0];
-      P[4 * c + 1] = q[1];
-      P[4 * c + 2] = q[2];
-      P[4 * c + 3] = q[3];
-    }
-  }
-  uint32_t info = 0u;
-  if (valid) {
-    const uint32_t marker = be16_lo(P[3]);
-    const uint32_t k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
-    const uint32_t eth_len = 14u + 4u * k;
-    const uint32_t et = be16_lo(sel3(k, P[3], P[4], P[5]));
-    uint32_t A[8];  // L3-relative dwords 0..6 (IPv4 header, TCP ports)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) A[j] = __builtin_amdgcn_alignbyte(P[4 + j], P[3 + j], 2);
-    uint32_t L[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) L[j] = sel3(k, A[j], j + 1 < 8 ? A[j + 1] : 0u, j + 2 < 8 ? A[j + 2] : 0u);
-    uint32_t disp = CGPU_ABORT, st;
-    if (len == 0u) st = CGPU_PKT_ETH_BAD_OFFSET;                 // parse::<Ethernet>()?
-    else if (len < eth_len) st = CGPU_PKT_ETH_OUT_OF_BUFFER;
-    else if (et != 0x0800u) st = CGPU_PKT_NOT_IPV4;              // parse::<Ipv4>()?
-    else if (eth_len >= len) st = CGPU_PKT_L3_BAD_OFFSET;
-    else if (eth_len + 20u > len) st = CGPU_PKT_L3_OUT_OF_BUFFER;
-    else {
-      st = CGPU_PKT_OK;
-      disp = CGPU_DROP;
-      const uint32_t flags_frag = be16_hi(L[1]);  // flags/fragment offset: L3 bytes 6-7
-      const uint32_t proto = (L[2] >> 8) & 0xffu;
-      if (proto == 6u && (flags_frag & 0x1fffu) == 0u && !(flags_frag & 0x2000u)) {
-        const uint32_t tcp_off = eth_len + 20u;
-        if (tcp_off >= len) { st = CGPU_PKT_L4_BAD_OFFSET; disp = CGPU_ABORT; }   // peek::<Tcp4>()?
-        else if (tcp_off + 20u > len) { st = CGPU_PKT_L4_OUT_OF_BUFFER; disp = CGPU_ABORT; }
-        else {
-          const uint32_t gw_port = be16_hi(L[5]);  // TCP destination port (L3 bytes 22-23)
-          const uint64_t r = a.pm.rev[gw_port];
-          if (r != ~0ull) {  // assigned_addr(port) = Some((dst, port))
-            if (len >= kDataRoom - 20u) {  // push::<Ipv6>(): extend 40 needs 40 < tailroom
-              st = CGPU_PKT_NOT_RESIZED;
-              disp = CGPU_ABORT;
-            } else {
-              disp = CGPU_ACT;
-              const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[(uint32_t)r]);
-              const u32x4 s0 = sp[0], s1 = sp[1];
-              const uint32_t de = (L[0] >> 8) & 0xffu;             // dscp_ecn (v4.rs:186-203)
-              const uint32_t dscp = de >> 2, ecn = de & 3u;
-              const uint32_t hop = ((L[2] & 0xffu) - 1u) & 0xffu;   // ttl - 1 (u8, wrapping)
-              const uint32_t new_len = len + 20u;
-              // Ipv6Header::default + set_dscp/ecn/next_header/hop_limit/src/dst
-              const uint32_t w = (6u << 28) | ((dscp << 22) & 0x0fc00000u) | ((ecn << 20) & 0x00300000u);
-              const uint32_t V0 = be32(w);
-              const uint32_t V1 = swap16((new_len - eth_len - 40u) & 0xffffu) | (6u << 16) | (hop << 24);
-              const uint32_t V2 = 0x9bff6400u;  // 64:ff9b::/96 (map4to6, main.rs:62-74)
-              const uint32_t V5 = L[3];         // v4 source address
-              // V6..V9: the ADDR_MAP key, the original v6 source
-              uint32_t ph = 0;                  // v6 pseudo-header addresses, LE residue
-              ph = sad16(V2, ph);
-              ph = sad16(V5, ph);
-              ph = sad16(s0[1], sad16(s0[2], sad16(s0[3], sad16(s1[0], ph))));
-              info = k | kNow | (s1[1] << 16);  // the original v6-side port
-              lrec[t][0] = u32x4{off, a.out_off[i], new_len, info};
-              lrec[t][1] = u32x4{V0, V1, V2, 0u};
-              lrec[t][2] = u32x4{0u, V5, s0[1], s0[2]};
-              lrec[t][3] = u32x4{s0[3], s1[0], fold32(ph), 0u};
-            }
-          }
-        }
+  for (int j = 0; j < 6; ++j) v.L[j] = sel3(v.k, A[j], j + 1 < 8 ? A[j + 1] : 0u, j + 2 < 8 ? A[j + 2] : 0u);
+  v.disp = CGPU_ABORT;
+  v.gw_port = 0u;
+  if (len == 0u) v.st = CGPU_PKT_ETH_BAD_OFFSET;                 // parse::<Ethernet>()?
+  else if (len < v.eth_len) v.st = CGPU_PKT_ETH_OUT_OF_BUFFER;
+  else if (et != 0x0800u) v.st = CGPU_PKT_NOT_IPV4;              // parse::<Ipv4>()?
+  else if (v.eth_len >= len) v.st = CGPU_PKT_L3_BAD_OFFSET;
+  else if (v.eth_len + 20u > len) v.st = CGPU_PKT_L3_OUT_OF_BUFFER;
+  else {
+    v.st = CGPU_PKT_OK;
+    v.disp = CGPU_DROP;
+    const uint32_t flags_frag = be16_hi(v.L[1]);  // flags/fragment offset: L3 bytes 6-7
+    const uint32_t proto = (v.L[2] >> 8) & 0xffu;
+    if (proto == 6u && (flags_frag & 0x1fffu) == 0u && !(flags_frag & 0x2000u)) {
+      const uint32_t tcp_off = v.eth_len + 20u;
+      if (tcp_off >= len) { v.st = CGPU_PKT_L4_BAD_OFFSET; v.disp = CGPU_ABORT; }   // peek::<Tcp4>()?
+      else if (tcp_off + 20u > len) { v.st = CGPU_PKT_L4_OUT_OF_BUFFER; v.disp = CGPU_ABORT; }
+      else {
+        v.gw_port = be16_hi(v.L[5]);  // TCP destination port (L3 bytes 22-23)
+        v.disp = CGPU_ACT;            // pending the ADDR_MAP lookup
       }
     }
-    if (disp != CGPU_ACT) a.out_len[i] = 0;
-    a.disposition[i] = (uint8_t)disp;
-    a.status[i] = (uint8_t)st;
   }
-  if (!(info & kNow)) lrec[t][0] = u32x4{0u, 0u, 0u, 0u};
-  __syncthreads();
-  rewrite_block<false>(a, lrec);
+}
+
+__global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_4to6_fused(Nat64Args a) {
+  const uint32_t g = threadIdx.x & (kFG - 1u);
+  const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
+  const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
+  QuadDesc d = quad_desc<false>(a, blockIdx.x * (kBlock / kFG) + threadIdx.x / kFG);
+  quad_modes<false>(a, d);
+  const bool al16 = d.fast && !__ballot(d.nl != 0u && (d.off & 15u) != 0u);
+  u32x4 X[kFJ], Y, Y4;
+  uint32_t E;
+  issue_frame_loads<false>(rs, d, g, al16, X, E);
+  header_loads(rs, a.arena_len, d.off, g, d.valid, d.hdr_fast, d.al_wave, Y, Y4);
+  uint32_t P[20];
+  gather_header(Y, Y4, P);
+  V4 v;
+  classify4(P, d.len, v);
+  // assigned_addr(port) (main.rs:56-58): ADDR_MAP as the reverse array; the
+  // quad's lanes read the same words (one request per quad)
+  u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
+  if (d.valid && v.disp == CGPU_ACT) {
+    const uint64_t r = a.pm.rev[v.gw_port];
+    if (r == ~0ull) {
+      v.disp = CGPU_DROP;  // no mapping: Either::Drop
+    } else if (d.len >= kDataRoom - 20u) {  // push::<Ipv6>(): extend 40 needs 40 < tailroom
+      v.st = CGPU_PKT_NOT_RESIZED;
+      v.disp = CGPU_ABORT;
+    } else {
+      const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[(uint32_t)r]);
+      s0 = sp[0];
+      s1 = sp[1];
+    }
+  }
+  const bool act = d.valid && v.disp == CGPU_ACT;
+  if (d.valid && g == 0u) {
+    a.out_len[d.i] = act ? (uint16_t)d.nl : 0;
+    a.disposition[d.i] = (uint8_t)v.disp;
+    a.status[d.i] = (uint8_t)v.st;
+  }
+  if (!act) return;
+  FrameRec f;
+  f.in_off = d.off;
+  f.o_off = d.o_off;
+  f.new_len = d.nl;
+  const uint32_t de = (v.L[0] >> 8) & 0xffu;            // dscp_ecn (v4.rs:186-203)
+  const uint32_t dscp = de >> 2, ecn = de & 3u;
+  const uint32_t hop = ((v.L[2] & 0xffu) - 1u) & 0xffu;  // ttl - 1 (u8, wrapping)
+  // Ipv6Header::default + set_dscp/ecn/next_header/hop_limit/src/dst
+  const uint32_t w = (6u << 28) | ((dscp << 22) & 0x0fc00000u) | ((ecn << 20) & 0x00300000u);
+  f.V[0] = be32(w);
+  f.V[1] = swap16((d.nl - v.eth_len - 40u) & 0xffffu) | (6u << 16) | (hop << 24);
+  f.V[2] = 0x9bff6400u;  // 64:ff9b::/96 (map4to6, main.rs:62-74)
+  f.V[3] = 0u;
+  f.V[4] = 0u;
+  f.V[5] = v.L[3];       // v4 source address
+  // V6..V9: the ADDR_MAP key, the original v6 source
+  f.V[6] = s0[1];
+  f.V[7] = s0[2];
+  f.V[8] = s0[3];
+  f.V[9] = s1[0];
+  uint32_t ph = 0;       // v6 pseudo-header addresses, LE residue
+  ph = sad16(f.V[2], ph);
+  ph = sad16(f.V[5], ph);
+  ph = sad16(s0[1], sad16(s0[2], sad16(s0[3], sad16(s1[0], ph))));
+  f.ph = fold32(ph);
+  f.info = v.k | kNow | (s1[1] << 16);  // the original v6-side port
+  rewrite_quad<false>(a, rs, ors, g, d, al16, f, X, E);
 }
 
 __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
@@ -777,18 +1015,19 @@ hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStr
 hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const uint32_t nb = nat64_num_blocks(a.n);
-  const uint32_t nb5 = (a.n + kBlock / kFG - 1) / (kBlock / kFG);
-  hipLaunchKernelGGL(nat64_6to4_fused, dim3(nb), dim3(kBlock), 0, s, a);
+  const uint32_t nbq = (a.n + kBlock / kFG - 1) / (kBlock / kFG);  // one quad per frame
+  hipLaunchKernelGGL(nat64_6to4_fused, dim3(nbq), dim3(kBlock), 0, s, a);
   hipLaunchKernelGGL(nat64_count, dim3(nb), dim3(kBlock), 0, s, a);
   hipLaunchKernelGGL(nat64_scan, dim3(1), dim3(kScanBlock), 0, s, a, nb);
   hipLaunchKernelGGL(nat64_assign, dim3(nb), dim3(kBlock), 0, s, a);
-  hipLaunchKernelGGL(nat64_6to4_deferred, dim3(nb5 < 2048u ? nb5 : 2048u), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(nat64_6to4_deferred, dim3(nbq < 2048u ? nbq : 2048u), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_nat64_4to6(const Nat64Args &a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(nat64_4to6_fused, dim3(nat64_num_blocks(a.n)), dim3(kBlock), 0, s, a);
+  const uint32_t nbf = (a.n + kBlock / kFG - 1) / (kBlock / kFG);
+  hipLaunchKernelGGL(nat64_4to6_fused, dim3(nbf), dim3(kBlock), 0, s, a);  // one quad per frame
   return hipGetLastError();
 }
 

@@ -63,6 +63,40 @@ __global__ __launch_bounds__(256) void aos_window_aux(const uint8_t *arena, cons
   out[i] = s[0] ^ s[1] ^ s[2] ^ s[3];
 }
 
+// AoS without the descriptor dependency (offset = 64 i): bounds the cost of
+// the off[i] -> arena load chain
+__global__ __launch_bounds__(256) void aos_nodesc(const uint8_t *arena, uint32_t n, uint32_t *out) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(arena), (short)0, (int)(n * 64u), 0x00020000);
+  u32x4 s = {0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) s += __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(64u * i + 16u * c), 0, 0);
+  out[i] = s[0] ^ s[1] ^ s[2] ^ s[3];
+}
+
+// AoS, grid-stride over packet groups with the next group's descriptor and
+// window loads issued before the current group's are consumed
+template <int GRID>
+__global__ __launch_bounds__(256) void aos_loop(const uint8_t *arena, const uint32_t *off,
+                                                uint32_t n, uint32_t *out) {
+  auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(arena), (short)0, (int)(n * 64u), 0x00020000);
+  uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t stride = GRID * 256u;
+  uint32_t o = i < n ? off[i] : 0xffffff00u;
+  u32x4 v[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) v[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(o + 16u * c), 0, 0);
+  for (; i < n; i += stride) {
+    const uint32_t j = i + stride;
+    const uint32_t on = j < n ? off[j] : 0xffffff00u;
+    u32x4 s = v[0] + v[1] + v[2] + v[3];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(on + 16u * c), 0, 0);
+    out[i] = s[0] ^ s[1] ^ s[2] ^ s[3];
+  }
+}
+
 // LDS staging: the wave loads the 4 KiB span of its 64 packets coalesced
 // (lane L, instruction c -> bytes 1024c + 16L), writes it to LDS with the
 // 16-B chunk index XOR-swizzled by bits 8-9, then each lane reads its own 64 B.
@@ -110,6 +144,33 @@ __global__ __launch_bounds__(256) void copy_frames(const uint8_t *in, uint8_t *o
   for (int j = 0; j < 4; ++j) {
     const uint32_t c = 4u * g + j;
     __builtin_amdgcn_raw_buffer_store_b128(v[j], os, (int)(16u * c + 16u <= new_len ? p * 256u + 16u * c : 0xffffff00u), 0, 0);
+  }
+}
+
+// the nat64 6to4 shape on the copy_map mapping: 236-B output, chunks >= 2
+// read from input + 20 (dword-aligned, not 16-B aligned), last chunk b96
+template <int G, int AUX>
+__global__ __launch_bounds__(256) void copy_shift(const uint8_t *in, uint8_t *out, uint32_t n) {
+  constexpr int C = 16 / G;
+  const uint32_t g = threadIdx.x % G, p = blockIdx.x * (256 / G) + threadIdx.x / G;
+  if (p >= n) return;
+  auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(in), (short)0, (int)(n * 256u), 0x00020000);
+  auto os = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(n * 256u), 0x00020000);
+  u32x4 v[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    const uint32_t c = (uint32_t)j * G + g;
+    const uint32_t src = c < 2u ? 16u * c : 16u * c + 20u;
+    v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * c < 236u ? p * 256u + src : 0xffffff00u), 0, AUX);
+  }
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    const uint32_t c = (uint32_t)j * G + g;
+    if (16u * c + 16u <= 236u)
+      __builtin_amdgcn_raw_buffer_store_b128(v[j], os, (int)(p * 256u + 16u * c), 0, AUX);
+    else if (16u * c < 236u)
+      __builtin_amdgcn_raw_buffer_store_b96(__builtin_shufflevector(v[j], v[j], 0, 1, 2), os,
+                                            (int)(p * 256u + 16u * c), 0, AUX);
   }
 }
 
@@ -219,6 +280,14 @@ int main(int argc, char **argv) {
                        off[r], n, scratch);                                                   \
   });
   AOSAUX(0) AOSAUX(1) AOSAUX(2) AOSAUX(3)
+  time_it("aos_nodesc64", algo - 6.0 * n, [&](int r) {
+    hipLaunchKernelGGL(aos_nodesc, dim3((n + 255) / 256), dim3(256), 0, st, arena[r], n, scratch);
+  });
+#define AOSLOOP(G)                                                                          \
+  time_it("aos_loop64_grid" #G, algo - 2.0 * n, [&](int r) {                                \
+    hipLaunchKernelGGL(aos_loop<G>, dim3(G), dim3(256), 0, st, arena[r], off[r], n, scratch); \
+  });
+  AOSLOOP(1024) AOSLOOP(2048) AOSLOOP(4096)
   time_it("lds_window64", algo - 2.0 * n, [&](int r) {
     hipLaunchKernelGGL(lds_window, dim3((n + 255) / 256), dim3(256), 0, st, arena[r], off[r], n,
                        scratch);
@@ -263,6 +332,12 @@ int main(int argc, char **argv) {
     MAPCASE(1, false, 0) MAPCASE(2, false, 0) MAPCASE(4, false, 0) MAPCASE(4, true, 0)
     MAPCASE(8, true, 0) MAPCASE(16, true, 0) MAPCASE(16, true, 2) MAPCASE(4, true, 2)
     MAPCASE(16, true, 1)
+#define SHIFTCASE(G, AUX)                                                                   \
+  time_it("copy_shift20_G" #G "_aux" #AUX, (double)nf * (256 + 236), [&](int r) {             \
+    hipLaunchKernelGGL((copy_shift<G, AUX>), dim3((nf * G + 255) / 256), dim3(256), 0, st,    \
+                       fin[r % 4], fout, nf);                                               \
+  });
+    SHIFTCASE(4, 0) SHIFTCASE(8, 0) SHIFTCASE(16, 0) SHIFTCASE(16, 2) SHIFTCASE(4, 2)
     time_it("copy_frames_shift0_256B", (double)nf * 512, [&](int r) {
       hipLaunchKernelGGL(copy_frames<0>, dim3((nf + 63) / 64), dim3(256), 0, st, fin[r % 4], fout, nf, 256u);
     });
