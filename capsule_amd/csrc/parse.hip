@@ -126,10 +126,27 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       P[4 * c + 2] = v[2];
       P[4 * c + 3] = v[3];
     }
+    // Bytes 64..95, per lane: with an L4 checksum every frame that reaches a
+    // chunk needs it; without, only frames whose headers end past byte 64
+    // (IPv6/TCP, or IPv6 behind VLAN tags) -- decided from the first 64 B, so
+    // every other frame stays at one 64-B segment.  An instruction is skipped
+    // when no lane of the wave needs it.
+    uint32_t hdr_end = 96u;
+    if (!L4C) {
+      const uint32_t mk = be16_lo(P[3]);
+      const uint32_t kk = mk == 0x8100u ? 1u : (mk == 0x88a8u ? 2u : 0u);
+      const uint32_t et = be16_lo(sel3(kk, P[3], P[4], P[5]));
+      const uint32_t w5 = sel3(kk, P[5], P[6], P[7]);  // normalized bytes 20..23
+      const bool is6 = et == 0x86ddu;
+      const uint32_t pr = is6 ? (w5 & 0xffu) : (w5 >> 24);
+      hdr_end = (is6 ? 54u + 4u * kk : 0u) + (pr == 6u ? 20u : 8u);
+    }
 #pragma unroll
     for (int c = 4; c < 6; ++c) {
+      const bool need = len > 16u * c && hdr_end > 16u * c;
       u32x4 v = {0u, 0u, 0u, 0u};
-      if (__ballot(len > 16u * c)) v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u * c), 0, 0);
+      if (__ballot(need))
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(need ? off + 16u * c : kNoRead), 0, 0);
       P[4 * c] = v[0];
       P[4 * c + 1] = v[1];
       P[4 * c + 2] = v[2];
