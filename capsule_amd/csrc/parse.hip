@@ -33,7 +33,10 @@ namespace cgpu {
 
 namespace {
 
-constexpr uint32_t kBlock = 256;
+#ifndef CGPU_PARSE_BLOCK
+#define CGPU_PARSE_BLOCK 256
+#endif
+constexpr uint32_t kBlock = CGPU_PARSE_BLOCK;
 constexpr int kWin = 24;        // packet-relative window dwords (96 B)
 constexpr uint32_t kQEnd = 88;  // normalized window bytes valid after a QinQ shift
 constexpr uint32_t kNoRead = 0xffffff00u;  // > any arena_len the ABI accepts
