@@ -214,6 +214,10 @@ def main():
                          "slower than direct launches on MI355X: kept for comparison)")
     ap.add_argument("--e2e", action="store_true",
                     help="host-resident batches: pinned H2D + parse + D2H, pipelined (DESIGN.md §8)")
+    ap.add_argument("--ingress", choices=["stage", "zero_copy"],
+                    help="with --e2e: rte_mbuf bursts from a host mempool through cgpu_parse_mbufs")
+    ap.add_argument("--burst", type=int, default=1 << 18,
+                    help="with --ingress: mbufs per cgpu_parse_mbufs call")
     args = ap.parse_args()
 
     import torch
@@ -222,6 +226,8 @@ def main():
     from capsule_amd import packets
     from capsule_amd.shards import ShardGroup
 
+    if args.e2e and args.ingress:
+        return e2e_mbufs(args)
     if args.e2e:
         return e2e(args)
     g = ShardGroup()
@@ -353,6 +359,57 @@ def main():
         print(json.dumps(result), flush=True)
     ctx.close()
     g.close()
+
+
+def e2e_mbufs(args):
+    """End-to-end rate of rte_mbuf bursts: a DPDK-style mempool of the parse
+    workload's frames in page-locked host memory, bursts of --burst mbuf
+    pointers through cgpu_parse_mbufs (synchronous: gather -> parse -> results
+    in host arrays), one core, one stream.  Prints one JSON line."""
+    import torch
+
+    from capsule_amd import _native as N
+    from capsule_amd import packets, synth
+
+    torch.cuda.set_device(0)
+    w = make_workload(args.config, 0xC0FFEE + 2)
+    if w["kind"] != "parse":
+        raise SystemExit("--ingress applies to the parse configs")
+    n = len(w["off"])
+    ctx = packets.Context(0)
+    stride = (128 + 128 + int(w["len"].max()) + 63) // 64 * 64
+    pinned = torch.zeros(stride * n, dtype=torch.uint8, pin_memory=True)
+    mem, mbufs = synth.mbuf_pool(w["arena"], w["off"], w["len"], mem=pinned.numpy())
+    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    ingress = {"stage": N.INGRESS_STAGE, "zero_copy": N.INGRESS_ZERO_COPY}[args.ingress]
+    B = min(args.burst, n)
+    bursts = [mbufs[s:s + B] for s in range(0, n - B + 1, B)]
+    outs = [(np.zeros(B, np.uint32), np.zeros(B, np.uint64)) for _ in range(2)]
+    L = N.lib()
+
+    def call(k):
+        mb = bursts[k % len(bursts)]
+        meta, fh = outs[k & 1]
+        N.check(L.cgpu_parse_mbufs(ctx.handle, mb.ctypes.data, B, w["flags"], ingress,
+                                   meta.ctypes.data, None, fh.ctypes.data, None),
+                "cgpu_parse_mbufs")
+
+    for k in range(3):
+        call(k)
+    calls, t0 = 0, time.perf_counter()
+    while calls < max(4, args.steps // 10) or time.perf_counter() - t0 < 2.0:
+        call(calls)
+        calls += 1
+    el = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": "end-to-end Mpps, rte_mbuf bursts from a host mempool (cgpu_parse_mbufs)",
+        "value": round(calls * B / el / 1e6, 2), "unit": "Mpps", "config": args.config,
+        "ingress": args.ingress, "burst": B, "calls": calls,
+        "us_per_burst": round(el / calls * 1e6, 1),
+        "mempool": f"{n} objects x {stride} B, page-locked, shuffled; 128-B rte_mbuf headers"}),
+        flush=True)
+    reg.close()
+    ctx.close()
 
 
 def e2e(args):

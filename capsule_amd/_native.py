@@ -14,7 +14,7 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ.get("CAPSULE_GPU_LIB", _HERE / "libcapsule_gpu.so"))
 
 # ---- constants (include/capsule_gpu.h) ------------------------------------
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 OK, EINVAL, ENOMEM, ENODEV, EIO, ENOSPC = 0, -22, -12, -19, -5, -28
 
@@ -42,6 +42,10 @@ F_CSUM_L4 = 1 << 5
 F_FLOW_HASH = 1 << 6
 
 ACT, DROP, ABORT = 0, 1, 2
+
+# rte_mbuf ingress (include/capsule_gpu.h; DPDK 19.11 field offsets)
+MBUF_BUF_ADDR_OFF, MBUF_DATA_OFF_OFF, MBUF_DATA_LEN_OFF, MBUF_SIZE = 0, 16, 40, 128
+INGRESS_STAGE, INGRESS_ZERO_COPY = 0, 1
 
 KEY_U8, KEY_META_CLASS = 0, 1
 
@@ -101,7 +105,8 @@ EXPORTS = [
     "cgpu_ctx_create", "cgpu_ctx_destroy", "cgpu_parse_batch", "cgpu_parse_host",
     "cgpu_portmap_create", "cgpu_portmap_destroy", "cgpu_portmap_next_port",
     "cgpu_portmap_size", "cgpu_nat64_6to4", "cgpu_nat64_4to6", "cgpu_group_by", "cgpu_last_error", "cgpu_strerror",
-    "cgpu_pkt_status_str", "cgpu_abi_version",
+    "cgpu_pkt_status_str", "cgpu_abi_version", "cgpu_host_register", "cgpu_host_unregister",
+    "cgpu_parse_mbufs",
 ]
 
 _lib = None
@@ -145,6 +150,12 @@ def lib():
     L.cgpu_nat64_6to4.argtypes = [vp, vp, P(Batch), vp, ctypes.c_uint64, vp, vp, vp, vp, vp]
     L.cgpu_nat64_4to6.restype = i32
     L.cgpu_nat64_4to6.argtypes = [vp, vp, P(Batch), vp, ctypes.c_uint64, vp, vp, vp, vp, vp]
+    L.cgpu_host_register.restype = i32
+    L.cgpu_host_register.argtypes = [vp, vp, ctypes.c_size_t]
+    L.cgpu_host_unregister.restype = i32
+    L.cgpu_host_unregister.argtypes = [vp, vp]
+    L.cgpu_parse_mbufs.restype = i32
+    L.cgpu_parse_mbufs.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp, vp]
     L.cgpu_group_by.restype = i32
     L.cgpu_group_by.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp]
     if L.cgpu_abi_version() != ABI_VERSION:

@@ -46,6 +46,10 @@ struct cgpu_ctx {
   size_t desc_cap = 0;
   uint32_t *gb_counts = nullptr;  // cgpu_group_by scratch
   size_t gb_cap = 0;              // entries
+  // host regions registered for zero-copy ingress
+  cgpu::HostRegion reg[cgpu::kMaxRegions];
+  bool reg_owned[cgpu::kMaxRegions];  // registered here (else: already page-locked)
+  uint32_t nreg = 0;
 };
 
 struct cgpu_portmap {
@@ -127,6 +131,8 @@ void cgpu_ctx_destroy(cgpu_ctx *c) {
   if (c->h_desc) (void)hipHostFree(c->h_desc);
   if (c->d_desc) (void)hipFree(c->d_desc);
   if (c->gb_counts) (void)hipFree(c->gb_counts);
+  for (uint32_t r = 0; r < c->nreg; ++r)
+    if (c->reg_owned[r]) (void)hipHostUnregister((void *)(uintptr_t)c->reg[r].host_base);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -183,67 +189,233 @@ static int grow(uint8_t **h, uint8_t **d, size_t *cap, size_t need) {
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+
+}  // extern "C"
+
+// Output layout of the per-context descriptor staging for n packets.
+struct HostLayout {
+  size_t off, len, meta, csum, hash, fields, end;
+  HostLayout(uint32_t n, bool with_fields, size_t base = 0) {
+    off = base;
+    len = off + align_up(4ull * n, 256);
+    meta = len + align_up(2ull * n, 256);
+    csum = meta + align_up(4ull * n, 256);
+    hash = csum + align_up(4ull * n, 256);
+    fields = hash + align_up(8ull * n, 256);
+    end = fields + (with_fields ? align_up(sizeof(cgpu_hdr_record) * (size_t)n, 256) : 0);
+  }
+};
+
+// Parse the device batch described by `lay` inside ctx->d_desc and copy the
+// outputs to the caller's host arrays at packet index `at`; asynchronous.
+static int parse_and_return(cgpu_ctx *ctx, const uint8_t *arena, size_t arena_len, uint32_t n,
+                            const HostLayout &lay, uint32_t flags, uint32_t *meta, uint32_t *csum,
+                            uint64_t *flow_hash, cgpu_hdr_record *fields, uint32_t at) {
+  hipStream_t s = ctx->stream;
+  cgpu_batch b;
+  b.arena = arena;
+  b.arena_len = arena_len;
+  b.off = (const uint32_t *)(ctx->d_desc + lay.off);
+  b.len = (const uint16_t *)(ctx->d_desc + lay.len);
+  b.n = n;
+  cgpu_parse_out o;
+  o.meta = (uint32_t *)(ctx->d_desc + lay.meta);
+  o.csum = (uint32_t *)(ctx->d_desc + lay.csum);
+  o.flow_hash = (uint64_t *)(ctx->d_desc + lay.hash);
+  o.fields = fields ? (cgpu_hdr_record *)(ctx->d_desc + lay.fields) : nullptr;
+  if (!csum) flags &= ~(CGPU_F_CSUM_IP | CGPU_F_CSUM_L4);
+  if (!flow_hash) flags &= ~CGPU_F_FLOW_HASH;
+  if (int e = cgpu_parse_batch(ctx, &b, flags, &o, s)) return e;
+  if (hipMemcpyAsync(meta + at, o.meta, 4ull * n, hipMemcpyDeviceToHost, s) != hipSuccess)
+    return fail(CGPU_EIO);
+  if (csum && hipMemcpyAsync(csum + at, o.csum, 4ull * n, hipMemcpyDeviceToHost, s) != hipSuccess)
+    return fail(CGPU_EIO);
+  if (flow_hash &&
+      hipMemcpyAsync(flow_hash + at, o.flow_hash, 8ull * n, hipMemcpyDeviceToHost, s) != hipSuccess)
+    return fail(CGPU_EIO);
+  if (fields && hipMemcpyAsync(fields + at, o.fields, sizeof(cgpu_hdr_record) * (size_t)n,
+                               hipMemcpyDeviceToHost, s) != hipSuccess)
+    return fail(CGPU_EIO);
+  return 0;
+}
+
+// The staged host path: `get(i, p, len)` names packet i's bytes (false: bad
+// pointer); the calling core gathers them into pinned staging at 64-byte
+// slots (the mbuf data room layout), one DMA copies the burst.  Synchronous.
+template <class Get>
+static int parse_staged(cgpu_ctx *ctx, uint32_t n, Get get, uint32_t flags, uint32_t *meta,
+                        uint32_t *csum, uint64_t *flow_hash, cgpu_hdr_record *fields) {
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
+  size_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t *p;
+    uint16_t l;
+    if (!get(i, p, l)) return fail(CGPU_EINVAL);
+    total += align_up(l, 64);
+  }
+  if (total >= (1ull << 32)) return fail(CGPU_EINVAL);
+  if (int e = grow(&ctx->h_arena, &ctx->d_arena, &ctx->arena_cap, total + 64)) return fail(e);
+  const HostLayout lay(n, fields != nullptr);
+  if (int e = grow(&ctx->h_desc, &ctx->d_desc, &ctx->desc_cap, lay.end)) return fail(e);
+  uint32_t *hoff = (uint32_t *)(ctx->h_desc + lay.off);
+  uint16_t *hlen = (uint16_t *)(ctx->h_desc + lay.len);
+  size_t pos = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t *p;
+    uint16_t l;
+    get(i, p, l);
+    hoff[i] = (uint32_t)pos;
+    hlen[i] = l;
+    if (l) memcpy(ctx->h_arena + pos, p, l);
+    pos += align_up(l, 64);
+  }
+  hipStream_t s = ctx->stream;
+  if (hipMemcpyAsync(ctx->d_arena, ctx->h_arena, pos ? pos : 1, hipMemcpyHostToDevice, s) !=
+      hipSuccess)
+    return fail(CGPU_EIO);
+  if (hipMemcpyAsync(ctx->d_desc, ctx->h_desc, lay.meta, hipMemcpyHostToDevice, s) != hipSuccess)
+    return fail(CGPU_EIO);
+  if (int e = parse_and_return(ctx, ctx->d_arena, pos ? pos : 1, n, lay, flags, meta, csum,
+                               flow_hash, fields, 0))
+    return e;
+  if (hipStreamSynchronize(s) != hipSuccess) return fail(CGPU_EIO);
+  return ok();
+}
+
+// rte_mbuf field reads (DPDK 19.11 layout, ffi/src/bindings_rustdoc.rs:6869-6898)
+static inline void mbuf_fields(const void *m, const uint8_t *&data, uint16_t &len) {
+  const uint8_t *b = (const uint8_t *)m;
+  uint8_t *buf_addr;
+  uint16_t data_off;
+  memcpy(&buf_addr, b + CGPU_MBUF_BUF_ADDR_OFF, sizeof buf_addr);
+  memcpy(&data_off, b + CGPU_MBUF_DATA_OFF_OFF, sizeof data_off);
+  memcpy(&len, b + CGPU_MBUF_DATA_LEN_OFF, sizeof len);
+  data = buf_addr + data_off;
+}
+
+// Zero-copy: the device gathers the burst from registered host memory,
+// in chunks of at most 2^20 mbufs (a chunk's arena stays below 4 GiB).
+static int parse_zero_copy(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32_t flags,
+                           uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
+                           cgpu_hdr_record *fields) {
+  if (ctx->nreg == 0) return fail(CGPU_EINVAL);
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
+  constexpr uint32_t kChunk = 1u << 20;
+  constexpr size_t kSlotMax = 2176;  // the mbuf buffer: 128 headroom + 2048 data room (align 64)
+  const uint32_t m0 = n < kChunk ? n : kChunk;
+  if (int e = grow(&ctx->h_arena, &ctx->d_arena, &ctx->arena_cap, (size_t)m0 * kSlotMax + 64))
+    return fail(e);
+  const size_t ptrs = 0, counters = align_up(8ull * m0, 256);
+  const HostLayout lay(m0, fields != nullptr, counters + 256);
+  if (int e = grow(&ctx->h_desc, &ctx->d_desc, &ctx->desc_cap, lay.end)) return fail(e);
+  hipStream_t s = ctx->stream;
+  uint32_t bad_total = 0;
+  for (uint32_t at = 0; at < n; at += m0) {
+    const uint32_t m = n - at < m0 ? n - at : m0;
+    memcpy(ctx->h_desc + ptrs, mbufs + at, 8ull * m);
+    if (hipMemcpyAsync(ctx->d_desc + ptrs, ctx->h_desc + ptrs, 8ull * m, hipMemcpyHostToDevice, s) !=
+            hipSuccess ||
+        hipMemsetAsync(ctx->d_desc + counters, 0, 8, s) != hipSuccess)
+      return fail(CGPU_EIO);
+    cgpu::GatherArgs g;
+    g.mbufs = (const uint64_t *)(ctx->d_desc + ptrs);
+    g.n = m;
+    g.nreg = ctx->nreg;
+    for (uint32_t r = 0; r < cgpu::kMaxRegions; ++r) g.reg[r] = ctx->reg[r];
+    g.arena = ctx->d_arena;
+    g.off = (uint32_t *)(ctx->d_desc + lay.off);
+    g.len = (uint16_t *)(ctx->d_desc + lay.len);
+    g.cursor = (uint32_t *)(ctx->d_desc + counters);
+    g.bad = g.cursor + 1;
+    if (cgpu::launch_mbuf_gather(g, s) != hipSuccess) return fail(CGPU_EIO);
+    if (int e = parse_and_return(ctx, ctx->d_arena, (size_t)m * kSlotMax + 64, m, lay, flags, meta,
+                                 csum, flow_hash, fields, at))
+      return e;
+    uint32_t *hcnt = (uint32_t *)(ctx->h_desc + counters);
+    if (hipMemcpyAsync(hcnt, ctx->d_desc + counters, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return fail(CGPU_EIO);
+    bad_total += hcnt[1];
+  }
+  return bad_total ? fail(CGPU_EINVAL) : ok();
+}
+
+extern "C" {
+
 int cgpu_parse_host(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *len, uint32_t n,
                     uint32_t flags, uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
                     cgpu_hdr_record *fields) {
   if (!ctx) return fail(CGPU_EINVAL);
   if (n == 0) return ok();
   if (!pkt || !len || !meta) return fail(CGPU_EINVAL);
+  auto get = [&](uint32_t i, const uint8_t *&p, uint16_t &l) {
+    p = pkt[i];
+    l = len[i];
+    return p != nullptr || l == 0;
+  };
+  return parse_staged(ctx, n, get, flags, meta, csum, flow_hash, fields);
+}
+
+int cgpu_host_register(cgpu_ctx *ctx, void *base, size_t bytes) {
+  if (!ctx || !base || bytes == 0 || ctx->nreg >= cgpu::kMaxRegions) return fail(CGPU_EINVAL);
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
-  // Gather into pinned staging at 64-byte slots (the mbuf data room layout).
-  size_t total = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    if (!pkt[i] && len[i]) return fail(CGPU_EINVAL);
-    total += align_up(len[i], 64);
+  // Memory that is already page-locked (hipHostMalloc'd, or registered by
+  // someone else) is only mapped; anything else is registered here.
+  hipPointerAttribute_t attr;
+  const bool locked = hipPointerGetAttributes(&attr, base) == hipSuccess &&
+                      attr.type == hipMemoryTypeHost;
+  (void)hipGetLastError();
+  const bool owned = !locked;
+  if (owned && hipHostRegister(base, bytes, hipHostRegisterMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(CGPU_ENOMEM);
   }
-  if (total >= (1ull << 32)) return fail(CGPU_EINVAL);
-  if (int e = grow(&ctx->h_arena, &ctx->d_arena, &ctx->arena_cap, total + 64)) return fail(e);
-  const size_t o_off = 0, o_len = align_up(4ull * n, 256), o_meta = o_len + align_up(2ull * n, 256);
-  const size_t o_csum = o_meta + align_up(4ull * n, 256), o_hash = o_csum + align_up(4ull * n, 256);
-  const size_t o_fields = o_hash + align_up(8ull * n, 256);
-  const size_t dbytes = o_fields + (fields ? sizeof(cgpu_hdr_record) * (size_t)n : 0);
-  if (int e = grow(&ctx->h_desc, &ctx->d_desc, &ctx->desc_cap, dbytes)) return fail(e);
-  uint32_t *hoff = (uint32_t *)(ctx->h_desc + o_off);
-  uint16_t *hlen = (uint16_t *)(ctx->h_desc + o_len);
-  size_t pos = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    hoff[i] = (uint32_t)pos;
-    hlen[i] = len[i];
-    if (len[i]) memcpy(ctx->h_arena + pos, pkt[i], len[i]);
-    pos += align_up(len[i], 64);
+  void *dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, base, 0) != hipSuccess || !dev) {
+    if (owned) (void)hipHostUnregister(base);
+    return fail(CGPU_EIO);
   }
-  hipStream_t s = ctx->stream;
-  if (hipMemcpyAsync(ctx->d_arena, ctx->h_arena, pos ? pos : 1, hipMemcpyHostToDevice, s) !=
-      hipSuccess)
-    return fail(CGPU_EIO);
-  if (hipMemcpyAsync(ctx->d_desc, ctx->h_desc, o_meta, hipMemcpyHostToDevice, s) != hipSuccess)
-    return fail(CGPU_EIO);
-  cgpu_batch b;
-  b.arena = ctx->d_arena;
-  b.arena_len = pos ? pos : 1;
-  b.off = (const uint32_t *)(ctx->d_desc + o_off);
-  b.len = (const uint16_t *)(ctx->d_desc + o_len);
-  b.n = n;
-  cgpu_parse_out o;
-  o.meta = (uint32_t *)(ctx->d_desc + o_meta);
-  o.csum = (uint32_t *)(ctx->d_desc + o_csum);
-  o.flow_hash = (uint64_t *)(ctx->d_desc + o_hash);
-  o.fields = fields ? (cgpu_hdr_record *)(ctx->d_desc + o_fields) : nullptr;
-  if (!csum) flags &= ~(CGPU_F_CSUM_IP | CGPU_F_CSUM_L4);
-  if (!flow_hash) flags &= ~CGPU_F_FLOW_HASH;
-  if (int e = cgpu_parse_batch(ctx, &b, flags, &o, s)) return e;
-  if (hipMemcpyAsync(meta, o.meta, 4ull * n, hipMemcpyDeviceToHost, s) != hipSuccess)
-    return fail(CGPU_EIO);
-  if (csum && hipMemcpyAsync(csum, o.csum, 4ull * n, hipMemcpyDeviceToHost, s) != hipSuccess)
-    return fail(CGPU_EIO);
-  if (flow_hash &&
-      hipMemcpyAsync(flow_hash, o.flow_hash, 8ull * n, hipMemcpyDeviceToHost, s) != hipSuccess)
-    return fail(CGPU_EIO);
-  if (fields && hipMemcpyAsync(fields, o.fields, sizeof(cgpu_hdr_record) * (size_t)n,
-                               hipMemcpyDeviceToHost, s) != hipSuccess)
-    return fail(CGPU_EIO);
-  if (hipStreamSynchronize(s) != hipSuccess) return fail(CGPU_EIO);
+  cgpu::HostRegion &r = ctx->reg[ctx->nreg];
+  r.host_base = (uint64_t)(uintptr_t)base;
+  r.dev_base = (uint64_t)(uintptr_t)dev;
+  r.bytes = bytes;
+  ctx->reg_owned[ctx->nreg] = owned;
+  ++ctx->nreg;
   return ok();
+}
+
+int cgpu_host_unregister(cgpu_ctx *ctx, void *base) {
+  if (!ctx || !base) return fail(CGPU_EINVAL);
+  for (uint32_t r = 0; r < ctx->nreg; ++r) {
+    if (ctx->reg[r].host_base != (uint64_t)(uintptr_t)base) continue;
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
+    if (ctx->reg_owned[r] && hipHostUnregister(base) != hipSuccess) return fail(CGPU_EIO);
+    for (uint32_t q = r + 1; q < ctx->nreg; ++q) {
+      ctx->reg[q - 1] = ctx->reg[q];
+      ctx->reg_owned[q - 1] = ctx->reg_owned[q];
+    }
+    --ctx->nreg;
+    ctx->reg[ctx->nreg] = cgpu::HostRegion{0, 0, 0};
+    return ok();
+  }
+  return fail(CGPU_EINVAL);
+}
+
+int cgpu_parse_mbufs(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32_t flags,
+                     uint32_t ingress, uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
+                     cgpu_hdr_record *fields) {
+  if (!ctx) return fail(CGPU_EINVAL);
+  if (n == 0) return ok();
+  if (!mbufs || !meta) return fail(CGPU_EINVAL);
+  if (ingress == CGPU_INGRESS_ZERO_COPY)
+    return parse_zero_copy(ctx, mbufs, n, flags, meta, csum, flow_hash, fields);
+  if (ingress != CGPU_INGRESS_STAGE) return fail(CGPU_EINVAL);
+  auto get = [&](uint32_t i, const uint8_t *&p, uint16_t &l) {
+    if (!mbufs[i]) return false;
+    mbuf_fields(mbufs[i], p, l);
+    return p != nullptr || l == 0;
+  };
+  return parse_staged(ctx, n, get, flags, meta, csum, flow_hash, fields);
 }
 
 int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_port,

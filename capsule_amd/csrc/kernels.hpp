@@ -77,6 +77,24 @@ hipError_t launch_nat64_4to6(const Nat64Args &a, hipStream_t s);
 hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStream_t s);
 uint32_t nat64_num_blocks(uint32_t n);
 
+// ---- zero-copy rte_mbuf ingress (ingress.hip) ------------------------------
+struct HostRegion {
+  uint64_t host_base, dev_base, bytes;
+};
+constexpr uint32_t kMaxRegions = 16;
+struct GatherArgs {
+  const uint64_t *mbufs;  // [n] host rte_mbuf addresses (device copy of the array)
+  uint32_t n;
+  uint32_t nreg;
+  HostRegion reg[kMaxRegions];
+  uint8_t *arena;         // device arena, 64-B slots
+  uint32_t *off;          // [n]
+  uint16_t *len;          // [n]
+  uint32_t *cursor;       // slot allocation cursor (zero before the launch)
+  uint32_t *bad;          // mbufs / frames outside every registered region
+};
+hipError_t launch_mbuf_gather(const GatherArgs &g, hipStream_t s);
+
 // ---- group_by --------------------------------------------------------------
 struct GroupByArgs {
   const void *key;     // u8 arm keys or u32 meta words (kind)

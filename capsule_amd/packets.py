@@ -214,6 +214,41 @@ def parse_host(ctx, frames, flags=None, fields=False):
     return meta, csum, fh, recs
 
 
+class HostRegion:
+    """A host memory range registered for zero-copy ingress (a mempool's
+    memzone); unregistered on close()."""
+
+    def __init__(self, ctx, base, nbytes):
+        self.ctx, self.base = ctx, base
+        N.check(N.lib().cgpu_host_register(ctx.handle, base, nbytes), "cgpu_host_register")
+
+    def close(self):
+        if self.base is not None:
+            N.check(N.lib().cgpu_host_unregister(self.ctx.handle, self.base), "cgpu_host_unregister")
+            self.base = None
+
+
+def parse_mbufs(ctx, mbufs, flags=None, ingress=N.INGRESS_STAGE, fields=False):
+    """A burst of rte_mbufs (u64 numpy array of their addresses, the
+    Vec<Mbuf> of PacketRx::receive) parsed into host arrays.  ingress:
+    INGRESS_STAGE (the calling core gathers into pinned staging) or
+    INGRESS_ZERO_COPY (the device reads the registered mempool)."""
+    if flags is None:
+        flags = parse_flags()
+    mbufs = np.ascontiguousarray(mbufs, dtype=np.uint64)
+    n = len(mbufs)
+    meta = np.zeros(n, np.uint32)
+    csum = np.zeros(n, np.uint32)
+    fh = np.zeros(n, np.uint64)
+    fl = np.zeros((n, N.HDR_RECORD_SIZE), np.uint8) if fields else None
+    rc = N.lib().cgpu_parse_mbufs(
+        ctx.handle, mbufs.ctypes.data, n, flags, ingress, meta.ctypes.data, csum.ctypes.data,
+        fh.ctypes.data, fl.ctypes.data if fields else None)
+    N.check(rc, "cgpu_parse_mbufs")
+    recs = fl.view(np.dtype(N.HDR_RECORD_FIELDS)).reshape(-1) if fields else None
+    return meta, csum, fh, recs
+
+
 class Groups:
     """Result of `group_by`: `idx[off[k]:off[k+1]]` are arm k's packets."""
 

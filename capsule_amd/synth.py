@@ -294,3 +294,42 @@ def nat64_replies(out_arena, off, out_len):
         x, y = a[i + lo].copy(), a[i + hi].copy()
         a[i + lo], a[i + hi] = y, x
     return a, off.astype(np.uint32), out_len.astype(np.uint16)
+
+
+def mbuf_pool(arena, off, length, mem=None, headroom=128, seed=7):
+    """Lay a batch out as a DPDK-style mempool in host memory: one object per
+    packet = a 128-B rte_mbuf header (buf_addr @0, data_off @16, data_len
+    @40; DPDK 19.11 offsets) followed by its buffer (headroom + frame), object
+    stride a multiple of 64, objects in shuffled order (a pool hands out
+    buffers in no particular order).  `mem`: a u8 array to build in (e.g. a
+    pinned torch tensor's numpy view), else a new numpy array.  Returns
+    (mem, mbufs u64[n] = the rte_mbuf addresses in batch order)."""
+    n = len(off)
+    length = np.asarray(length, dtype=np.int64)
+    room = int(length.max()) if n else 0
+    stride = (128 + headroom + room + 63) // 64 * 64
+    need = max(stride * n, 64)
+    if mem is None:
+        mem = np.zeros(need, np.uint8)
+    assert mem.nbytes >= need and mem.dtype == np.uint8
+    base = mem.ctypes.data
+    objs = np.random.default_rng(seed).permutation(n).astype(np.int64) * stride
+    mem[:need] = 0
+    buf = (np.uint64(base) + objs.astype(np.uint64) + np.uint64(128))
+    for b in range(8):
+        mem[objs + b] = ((buf >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.uint8)
+    mem[objs + 16] = headroom & 0xFF
+    mem[objs + 17] = headroom >> 8
+    mem[objs + 40] = (length & 0xFF).astype(np.uint8)
+    mem[objs + 41] = (length >> 8).astype(np.uint8)
+    src0 = np.asarray(off, dtype=np.int64)
+    dst0 = objs + 128 + headroom
+    for c in range(0, n, 1 << 16):  # frames, 64 Ki packets at a time
+        L = length[c:c + (1 << 16)]
+        T = int(L.sum())
+        if not T:
+            continue
+        start = np.repeat(np.cumsum(L) - L, L)
+        intra = np.arange(T, dtype=np.int64) - start
+        mem[np.repeat(dst0[c:c + (1 << 16)], L) + intra] = arena[np.repeat(src0[c:c + (1 << 16)], L) + intra]
+    return mem, (np.uint64(base) + objs.astype(np.uint64)).astype(np.uint64)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CGPU_ABI_VERSION 1
+#define CGPU_ABI_VERSION 2
 
 /* ---- call-level return codes (negative errno style) -------------------- */
 #define CGPU_OK 0
@@ -184,6 +184,43 @@ int cgpu_parse_batch(cgpu_ctx *ctx, const cgpu_batch *batch, uint32_t flags,
 int cgpu_parse_host(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *len,
                     uint32_t n, uint32_t flags, uint32_t *meta, uint32_t *csum,
                     uint64_t *flow_hash, cgpu_hdr_record *fields);
+
+/* ---- rte_mbuf bursts (the DPDK seam) -------------------------------------
+ * A burst as PacketRx::receive returns it (Vec<Mbuf>, batch/mod.rs:110-119,
+ * port.rs:149-205): an array of rte_mbuf pointers.  The library reads three
+ * fields of each rte_mbuf, at the DPDK 19.11 offsets pinned by the bindgen
+ * layout test (ffi/src/bindings_rustdoc.rs:6869-6898): buf_addr, data_off,
+ * data_len.  Only the first segment is read, like Mbuf::data_len and
+ * read_data (mbuf.rs:196, 313-327).  The mbufs are borrowed for the call
+ * (never freed or kept, mbuf.rs:467-479).                                   */
+#define CGPU_MBUF_BUF_ADDR_OFF 0
+#define CGPU_MBUF_DATA_OFF_OFF 16
+#define CGPU_MBUF_DATA_LEN_OFF 40
+#define CGPU_MBUF_SIZE 128
+
+/* Ingress modes.
+ *   STAGE:     the calling core gathers each frame into pinned staging
+ *              (64-B slots) and one DMA copies the burst to the device.
+ *   ZERO_COPY: the device reads the mbufs and their frames straight from
+ *              host memory over PCIe into HBM; every mbuf and data buffer
+ *              must lie in a region registered with cgpu_host_register (a
+ *              mempool's memzone).  A pointer outside every registered
+ *              region fails the call with CGPU_EINVAL (nothing is read
+ *              through it).                                                */
+#define CGPU_INGRESS_STAGE 0u
+#define CGPU_INGRESS_ZERO_COPY 1u
+
+/* Page-lock and map host memory [base, base + bytes) for the device (the
+ * mempool of mempool.rs:64-106); up to 16 regions per context.             */
+int cgpu_host_register(cgpu_ctx *ctx, void *base, size_t bytes);
+int cgpu_host_unregister(cgpu_ctx *ctx, void *base);
+
+/* Parse a burst of n rte_mbufs; outputs as cgpu_parse_host, into HOST
+ * arrays (csum / flow_hash / fields may be NULL).  Synchronous: the burst's
+ * results are in the host arrays when the call returns.                  */
+int cgpu_parse_mbufs(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32_t flags,
+                     uint32_t ingress, uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
+                     cgpu_hdr_record *fields);
 
 /* ---- examples/nat64 6to4 -------------------------------------------------
  * Stateful IPv6 -> IPv4 rewrite of examples/nat64/main.rs:121-150, with the
