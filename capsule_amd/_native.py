@@ -21,7 +21,7 @@ OK, EINVAL, ENOMEM, ENODEV, EIO, ENOSPC = 0, -22, -12, -19, -5, -28
 PKT_STATUS = [
     "OK", "ETH_BAD_OFFSET", "ETH_OUT_OF_BUFFER", "NOT_IPV4", "NOT_IPV6", "NOT_IP",
     "L3_BAD_OFFSET", "L3_OUT_OF_BUFFER", "NOT_UDP", "NOT_TCP", "NOT_L4", "L4_BAD_OFFSET",
-    "L4_OUT_OF_BUFFER", "NOT_RESIZED", "TABLE_FULL",
+    "L4_OUT_OF_BUFFER", "NOT_RESIZED", "TABLE_FULL", "NOT_ICMPV4", "NOT_ICMPV6",
 ]
 PKT = {name: i for i, name in enumerate(PKT_STATUS)}
 
@@ -30,7 +30,7 @@ META_L4_CSUM_OK = 1 << 21
 META_DOT1Q = 1 << 22
 META_QINQ = 1 << 23
 L3_NONE, L3_IPV4, L3_IPV6 = 0, 1, 2
-L4_NONE, L4_UDP, L4_TCP = 0, 1, 2
+L4_NONE, L4_UDP, L4_TCP, L4_ICMP = 0, 1, 2, 3
 
 F_ACCEPT_V4 = 1 << 0
 F_ACCEPT_V6 = 1 << 1
@@ -40,6 +40,7 @@ F_ACCEPT_ALL = 0xF
 F_CSUM_IP = 1 << 4
 F_CSUM_L4 = 1 << 5
 F_FLOW_HASH = 1 << 6
+F_ACCEPT_ICMP = 1 << 7  # not part of F_ACCEPT_ALL
 
 ACT, DROP, ABORT = 0, 1, 2
 

@@ -96,7 +96,9 @@ const char *cgpu_pkt_status_str(int s) {
     case CGPU_PKT_L3_OUT_OF_BUFFER: return "IP: out of buffer";
     case CGPU_PKT_NOT_UDP: return "not a UDP packet.";
     case CGPU_PKT_NOT_TCP: return "not a TCP packet.";
-    case CGPU_PKT_NOT_L4: return "not a UDP or TCP packet.";
+    case CGPU_PKT_NOT_L4: return "not a packet of an accepted L4 type.";
+    case CGPU_PKT_NOT_ICMPV4: return "not an ICMPv4 packet.";
+    case CGPU_PKT_NOT_ICMPV6: return "not an ICMPv6 packet.";
     case CGPU_PKT_L4_BAD_OFFSET: return "L4: bad offset";
     case CGPU_PKT_L4_OUT_OF_BUFFER: return "L4: out of buffer";
     case CGPU_PKT_NOT_RESIZED: return "buffer not resized";
@@ -152,14 +154,17 @@ int cgpu_parse_batch(cgpu_ctx *ctx, const cgpu_batch *batch, uint32_t flags,
   if (batch->n == 0) return ok();
   if (!out->meta) return fail(CGPU_EINVAL);
   if ((flags & CGPU_F_FLOW_HASH) && !out->flow_hash) return fail(CGPU_EINVAL);
-  if ((flags & CGPU_F_ACCEPT_ALL) == 0) flags |= CGPU_F_ACCEPT_ALL;
+  // no L3 (L4) type named: every IP version (UDP and TCP) accepted
+  if ((flags & (CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6)) == 0) flags |= CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6;
+  if ((flags & (CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP | CGPU_F_ACCEPT_ICMP)) == 0)
+    flags |= CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP;
   cgpu::ParseArgs a;
   a.arena = batch->arena;
   a.arena_len = (uint32_t)batch->arena_len;
   a.off = batch->off;
   a.len = batch->len;
   a.n = batch->n;
-  a.accept = flags & CGPU_F_ACCEPT_ALL;
+  a.accept = flags & (CGPU_F_ACCEPT_ALL | CGPU_F_ACCEPT_ICMP);
   a.meta = out->meta;
   a.csum = out->csum;
   a.hash = out->flow_hash;

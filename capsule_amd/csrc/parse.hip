@@ -25,6 +25,9 @@
 //   Tcp::compute_checksum      core/src/packets/tcp.rs:462-477
 //   PseudoHeader::sum          core/src/packets/checksum.rs:56-128
 //   Udp/Tcp::flow              core/src/packets/udp.rs:151-159, tcp.rs:409-417
+//   Icmpv4/Icmpv6::try_parse   core/src/packets/icmp/v4/mod.rs:205-220, icmp/v6/mod.rs:217-232 (4 B)
+//   Icmpv4::compute_checksum   icmp/v4/mod.rs:118-129 (no pseudo-header)
+//   Icmpv6::compute_checksum   icmp/v6/mod.rs:123-138 (pseudo-header, protocol 58)
 #include "capsule_gpu.h"
 #include "device_common.hpp"
 #include "kernels.hpp"
@@ -183,8 +186,10 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   const uint32_t proto = v6 ? (Q[5] & 0xffu) : (Q[5] >> 24);
   const bool udp = proto == 17u && (a.accept & CGPU_F_ACCEPT_UDP);
   const bool tcp = proto == 6u && (a.accept & CGPU_F_ACCEPT_TCP);
+  // ProtocolNumbers::Icmpv4 (1) under IPv4, Icmpv6 (58) under IPv6 (ip/mod.rs:41-75)
+  const bool icmp = proto == (v6 ? 58u : 1u) && (a.accept & CGPU_F_ACCEPT_ICMP);
   const uint32_t l4_off = eth_len + l3_len;
-  const uint32_t l4_len = udp ? 8u : 20u;
+  const uint32_t l4_len = udp ? 8u : (icmp ? 4u : 20u);
   uint32_t st = CGPU_PKT_OK;
   bool eth_ok = false, l3_ok = false;
   if (len == 0u) {
@@ -202,9 +207,13 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       st = CGPU_PKT_L3_OUT_OF_BUFFER;
     } else {
       l3_ok = true;
-      if (!udp && !tcp) {
-        const bool au = a.accept & CGPU_F_ACCEPT_UDP, at = a.accept & CGPU_F_ACCEPT_TCP;
-        st = (au && at) ? CGPU_PKT_NOT_L4 : (au ? CGPU_PKT_NOT_UDP : CGPU_PKT_NOT_TCP);
+      if (!udp && !tcp && !icmp) {
+        // exactly one accepted L4 type: its own error; several: NOT_L4
+        const uint32_t acc = a.accept & (CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP | CGPU_F_ACCEPT_ICMP);
+        st = acc == CGPU_F_ACCEPT_UDP    ? CGPU_PKT_NOT_UDP
+             : acc == CGPU_F_ACCEPT_TCP  ? CGPU_PKT_NOT_TCP
+             : acc == CGPU_F_ACCEPT_ICMP ? (v6 ? CGPU_PKT_NOT_ICMPV6 : CGPU_PKT_NOT_ICMPV4)
+                                         : CGPU_PKT_NOT_L4;
       } else if (l4_off >= len) {
         st = CGPU_PKT_L4_BAD_OFFSET;
       } else if (l4_off + l4_len > len) {
@@ -221,7 +230,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     if (k == 2u) meta |= CGPU_META_QINQ;
   }
   if (l3_ok) meta |= (v6 ? CGPU_L3_IPV6 : CGPU_L3_IPV4) << 16;
-  if (l4_ok) meta |= (udp ? CGPU_L4_UDP : CGPU_L4_TCP) << 18;
+  if (l4_ok) meta |= (udp ? CGPU_L4_UDP : (icmp ? CGPU_L4_ICMP : CGPU_L4_TCP)) << 18;
 
   // L4 header dwords (L4 starts at normalized byte 34 for v4, 54 for v6)
   uint32_t U[5];
@@ -256,9 +265,13 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     } else {
       s = sum_to_end<7>(Q, wend, s);
     }
-    stored_le = udp ? (v6 ? (Q[15] & 0xffffu) : (Q[10] & 0xffffu))
-                    : (v6 ? (Q[17] >> 16) : (Q[12] >> 16));
+    stored_le = udp    ? (v6 ? (Q[15] & 0xffffu) : (Q[10] & 0xffffu))
+                : icmp ? (v6 ? (Q[14] & 0xffffu) : (Q[9] & 0xffffu))
+                       : (v6 ? (Q[17] >> 16) : (Q[12] >> 16));
     s -= stored_le;
+    // ICMPv4 has no pseudo-header (icmp/v4/mod.rs:118-129): take the
+    // addresses (bytes 26..33) back out of the exact sum
+    if (icmp && !v6) s -= (Q[6] >> 16) + (Q[7] & 0xffffu) + (Q[7] >> 16) + (Q[8] & 0xffffu);
     has_tail = endn > kQEnd;  // span continues past the window
   }
   // Hash and header record first: only the checksum state stays live across
@@ -279,7 +292,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
 
   if (HASH) {
     uint64_t h = 0;
-    if (l4_ok) {  // Udp::flow / Tcp::flow (udp.rs:151-159, tcp.rs:409-417)
+    if (l4_ok && !icmp) {  // Udp::flow / Tcp::flow (udp.rs:151-159, tcp.rs:409-417); ICMP has none
       h = flow_hash(v6, src, dst, be16_lo(U[0]), be16_hi(U[0]), udp ? 17u : 6u);
     }
     if (valid) a.hash[i] = h;
@@ -319,7 +332,10 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
         R[14 + j] = dst[j];
       }
     }
-    if (l4_ok) {  // udp.rs:90-128, tcp.rs:139-405
+    if (l4_ok && icmp) {  // msg_type, code, checksum (icmp/v4/mod.rs:88-112, v6 :93-117)
+      R[18] = (U[0] & 0xffu) | (((U[0] >> 8) & 0xffu) << 16);
+      R[19] = be16_hi(U[0]) << 16;
+    } else if (l4_ok) {  // udp.rs:90-128, tcp.rs:139-405
       R[18] = be16_lo(U[0]) | (be16_hi(U[0]) << 16);
       if (udp) {
         R[19] = be16_lo(U[1]) | (be16_hi(U[1]) << 16);
@@ -408,7 +424,8 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   }
   if (L4C && l4_ok) {
     const uint32_t span = (len - l4_off) & 0xffffu;
-    l4_c = (~fold32(swap16(fold32(s)) + span + (udp ? 17u : 6u))) & 0xffffu;
+    if (icmp && !v6) l4_c = (~swap16(fold32(s))) & 0xffffu;  // compute(0, span)
+    else l4_c = (~fold32(swap16(fold32(s)) + span + (udp ? 17u : (icmp ? 58u : 6u)))) & 0xffffu;
     if (udp && l4_c == 0u) l4_c = 0xffffu;  // udp.rs:137-140
     if (l4_c == swap16(stored_le)) meta |= CGPU_META_L4_CSUM_OK;
   }

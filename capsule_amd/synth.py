@@ -15,10 +15,15 @@ aligned slots of a contiguous arena, the device image of a burst of mbufs.
 import numpy as np
 
 ETH_IPV4, ETH_IPV6 = 0x0800, 0x86DD
-UDP, TCP = 17, 6
+UDP, TCP, ICMP4, ICMP6 = 17, 6, 1, 58
 
 # kinds: (l3, l4) with l3 in {4, 6}, l4 in {UDP, TCP}
 V4_UDP, V4_TCP, V6_UDP, V6_TCP = (4, UDP), (4, TCP), (6, UDP), (6, TCP)
+V4_ICMP, V6_ICMP = (4, ICMP4), (6, ICMP6)  # 4-byte generic ICMP header
+
+
+def l4_header_len(l4):
+    return 8 if l4 == UDP else (20 if l4 == TCP else 4)
 
 
 def _fold(s):
@@ -57,7 +62,7 @@ def build_frames(rng, m, kind, frame_len, vlan=0, hop_limit_min=0):
     l3, l4 = kind
     eth_len = 14 + 4 * vlan
     l3_len = 20 if l3 == 4 else 40
-    l4_len = 8 if l4 == UDP else 20
+    l4_len = l4_header_len(l4)
     assert frame_len >= eth_len + l3_len + l4_len, (kind, frame_len)
     f = rng.integers(0, 256, size=(m, frame_len), dtype=np.uint8)  # random payload
     # Ethernet (strategy.rs:209-218): random dst/src MACs, ether_type implied.
@@ -95,12 +100,16 @@ def build_frames(rng, m, kind, frame_len, vlan=0, hop_limit_min=0):
     if l4 == UDP:
         _put16(f, t + 4, frame_len - t)  # reconcile: length (udp.rs:350-354)
         cs_at = t + 6
-    else:
+    elif l4 == TCP:
         cs_at = t + 16
+    else:  # ICMP checksum at +2 (icmp/v4/mod.rs:88-112)
+        cs_at = t + 2
     # L4 checksum over [t, frame_len) with the pseudo-header (checksum.rs).
     _put16(f, cs_at, 0)
     span = frame_len - t
-    if l3 == 4:
+    if l4 == ICMP4:  # Icmpv4::compute_checksum: no pseudo-header
+        ph = np.zeros(m, np.uint64)
+    elif l3 == 4:
         ph = _be_word_sum(f[:, o + 12 : o + 20]) + np.uint64(l4 + span)
     else:
         ph = _be_word_sum(f[:, o + 8 : o + 40]) + np.uint64(l4 + span)
@@ -239,11 +248,11 @@ def fuzz(n, seed=1, max_len=1600):
     """
     rng = np.random.default_rng(seed)
     frames = []
-    kinds = [V4_UDP, V4_TCP, V6_UDP, V6_TCP]
+    kinds = [V4_UDP, V4_TCP, V6_UDP, V6_TCP, V4_ICMP, V6_ICMP]
     for i in range(n):
-        kind = kinds[rng.integers(0, 4)]
+        kind = kinds[rng.integers(0, 4) if rng.random() < 0.8 else rng.integers(4, 6)]
         vlan = int(rng.integers(0, 3))
-        need = 14 + 4 * vlan + (20 if kind[0] == 4 else 40) + (8 if kind[1] == UDP else 20)
+        need = 14 + 4 * vlan + (20 if kind[0] == 4 else 40) + l4_header_len(kind[1])
         L = int(rng.integers(need, max(need + 1, max_len)))
         if rng.random() < 0.5:
             L = int(rng.integers(need, need + 64))

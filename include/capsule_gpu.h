@@ -59,20 +59,23 @@ enum cgpu_pkt_status {
   /* Udp/Tcp::try_parse (udp.rs:287-302, tcp.rs:558-573) */
   CGPU_PKT_NOT_UDP = 8,          /* "not a UDP packet."                      */
   CGPU_PKT_NOT_TCP = 9,          /* "not a TCP packet."                      */
-  CGPU_PKT_NOT_L4 = 10,          /* neither, when both were accepted        */
+  CGPU_PKT_NOT_L4 = 10,          /* none, when several L4 types were accepted */
   CGPU_PKT_L4_BAD_OFFSET = 11,
   CGPU_PKT_L4_OUT_OF_BUFFER = 12,
   /* nat64 only */
   CGPU_PKT_NOT_RESIZED = 13,     /* Mbuf::extend NotResized (mbuf.rs:225-233) */
   CGPU_PKT_TABLE_FULL = 14,      /* port table capacity exhausted            */
-  CGPU_PKT_STATUS_COUNT = 15
+  /* Icmpv4/Icmpv6::try_parse (icmp/v4/mod.rs:205-220, icmp/v6/mod.rs:217-232) */
+  CGPU_PKT_NOT_ICMPV4 = 15,      /* "not an ICMPv4 packet."                  */
+  CGPU_PKT_NOT_ICMPV6 = 16,      /* "not an ICMPv6 packet."                  */
+  CGPU_PKT_STATUS_COUNT = 17
 };
 
 /* ---- `meta` word layout (one u32 per packet) ---------------------------- */
 #define CGPU_META_STATUS(m) ((m) & 0xffu)        /* enum cgpu_pkt_status     */
 #define CGPU_META_ETH_LEN(m) (((m) >> 8) & 0xffu) /* 14 / 18 / 22, 0 if none  */
 #define CGPU_META_L3(m) (((m) >> 16) & 0x3u)      /* 0 none, 1 IPv4, 2 IPv6   */
-#define CGPU_META_L4(m) (((m) >> 18) & 0x3u)      /* 0 none, 1 UDP, 2 TCP     */
+#define CGPU_META_L4(m) (((m) >> 18) & 0x3u)      /* 0 none, 1 UDP, 2 TCP, 3 ICMP */
 #define CGPU_META_IP_CSUM_OK (1u << 20)           /* stored == computed       */
 #define CGPU_META_L4_CSUM_OK (1u << 21)           /* stored == computed       */
 #define CGPU_META_DOT1Q (1u << 22)                /* Ethernet::is_dot1q       */
@@ -83,6 +86,7 @@ enum cgpu_pkt_status {
 #define CGPU_L4_NONE 0u
 #define CGPU_L4_UDP 1u
 #define CGPU_L4_TCP 2u
+#define CGPU_L4_ICMP 3u /* ICMPv4 under IPv4, ICMPv6 under IPv6 */
 
 /* ---- parse flags --------------------------------------------------------
  * ACCEPT_* select which typed parses the caller would have written
@@ -97,6 +101,13 @@ enum cgpu_pkt_status {
 #define CGPU_F_CSUM_IP (1u << 4)   /* Ipv4::compute_checksum (v4.rs:322-333) */
 #define CGPU_F_CSUM_L4 (1u << 5)   /* Udp/Tcp::compute_checksum              */
 #define CGPU_F_FLOW_HASH (1u << 6) /* SipHash-1-3(0,0) of `Flow` */
+/* Also accept ICMPv4 (protocol 1) / ICMPv6 (next header 58) as the L4
+ * layer: Icmpv4/Icmpv6::try_parse, a 4-byte header; with CGPU_F_CSUM_L4 the
+ * checksum of Icmpv4::compute_checksum (no pseudo-header) / Icmpv6 (v6
+ * pseudo-header, protocol 58) over [l4 offset, data_len).  ICMP has no Flow:
+ * flow_hash is 0.  In the header record src_port = msg_type, dst_port =
+ * code, l4_checksum = the stored checksum.  Not part of CGPU_F_ACCEPT_ALL. */
+#define CGPU_F_ACCEPT_ICMP (1u << 7)
 
 /* ---- batch descriptor ---------------------------------------------------
  * A batch is an arena of packet bytes plus one (offset, data_len) pair per

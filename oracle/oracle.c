@@ -219,6 +219,7 @@ static void parse_one(const uint8_t *p, uint32_t len, uint32_t flags, uint32_t *
                       uint32_t *csum_out, uint64_t *hash_out, cgpu_hdr_record *rec) {
   const int acc4 = (flags & CGPU_F_ACCEPT_V4) != 0, acc6 = (flags & CGPU_F_ACCEPT_V6) != 0;
   const int accu = (flags & CGPU_F_ACCEPT_UDP) != 0, acct = (flags & CGPU_F_ACCEPT_TCP) != 0;
+  const int acci = (flags & CGPU_F_ACCEPT_ICMP) != 0;
   uint32_t meta = 0, ip_c = 0, l4_c = 0;
   uint64_t hash = 0;
   cgpu_hdr_record r;
@@ -293,16 +294,26 @@ static void parse_one(const uint8_t *p, uint32_t len, uint32_t flags, uint32_t *
     }
     meta |= (uint32_t)l3 << 16;
     l4_off = l3_off + l3_len;
-    /* Udp::try_parse (udp.rs:287-302) / Tcp::try_parse (tcp.rs:558-573) */
+    /* Udp::try_parse (udp.rs:287-302) / Tcp::try_parse (tcp.rs:558-573) /
+     * Icmpv4::try_parse (icmp/v4/mod.rs:205-220: protocol() == Icmpv4) /
+     * Icmpv6::try_parse (icmp/v6/mod.rs:217-232: next_protocol() == Icmpv6) */
     uint32_t l4_len = 0;
+    const uint8_t icmp_proto = l3 == CGPU_L3_IPV4 ? 0x01 : 0x3A; /* ip/mod.rs:41-75 */
     if (accu && proto == 17) {
       l4 = CGPU_L4_UDP;
       l4_len = 8;
     } else if (acct && proto == 6) {
       l4 = CGPU_L4_TCP;
       l4_len = 20; /* TcpHeader::size_of, tcp.rs:531-533 */
+    } else if (acci && proto == icmp_proto) {
+      l4 = CGPU_L4_ICMP;
+      l4_len = 4; /* Icmpv4Header / Icmpv6Header::size_of (icmp/v4/mod.rs:455) */
+    } else if (accu + acct + acci > 1) {
+      st = CGPU_PKT_NOT_L4;
     } else {
-      st = (accu && acct) ? CGPU_PKT_NOT_L4 : (accu ? CGPU_PKT_NOT_UDP : CGPU_PKT_NOT_TCP);
+      st = accu ? CGPU_PKT_NOT_UDP
+                : acct ? CGPU_PKT_NOT_TCP
+                       : (l3 == CGPU_L3_IPV4 ? CGPU_PKT_NOT_ICMPV4 : CGPU_PKT_NOT_ICMPV6);
     }
     if (!st)
       st = read_data(len, l4_off, l4_len, CGPU_PKT_L4_BAD_OFFSET, CGPU_PKT_L4_OUT_OF_BUFFER);
@@ -317,6 +328,11 @@ static void parse_one(const uint8_t *p, uint32_t len, uint32_t flags, uint32_t *
       r.udp_length_or_window = rd16(u + 4);
       r.l4_checksum = rd16(u + 6);
       cs_at = 6;
+    } else if (l4 == CGPU_L4_ICMP) { /* msg_type, code, checksum (icmp/v4/mod.rs:88-112) */
+      r.src_port = u[0];
+      r.dst_port = u[1];
+      r.l4_checksum = rd16(u + 2);
+      cs_at = 2;
     } else { /* tcp.rs:139-405 */
       r.seq_no = rd32(u + 4);
       r.ack_no = rd32(u + 8);
@@ -329,7 +345,7 @@ static void parse_one(const uint8_t *p, uint32_t len, uint32_t flags, uint32_t *
       cs_at = 16;
     }
     meta |= (uint32_t)l4 << 18;
-    const uint8_t pr = l4 == CGPU_L4_UDP ? 17 : 6; /* ProtocolNumbers::Udp / Tcp */
+    const uint8_t pr = l4 == CGPU_L4_UDP ? 17 : (l4 == CGPU_L4_ICMP ? 0x3A : 6); /* ip/mod.rs:41-75 */
     if (flags & CGPU_F_CSUM_L4) {
       /* Udp::compute_checksum (udp.rs:204-219) / Tcp (tcp.rs:462-477): the
        * span is [offset, data_len), checksum field zeroed first. */
@@ -338,7 +354,9 @@ static void parse_one(const uint8_t *p, uint32_t len, uint32_t flags, uint32_t *
       memcpy(data, u, span);
       wr16(data + cs_at, 0);
       uint16_t ph;
-      if (l3 == CGPU_L3_IPV4)
+      if (l4 == CGPU_L4_ICMP && l3 == CGPU_L3_IPV4)
+        ph = 0; /* Icmpv4::compute_checksum: compute(0, data) (icmp/v4/mod.rs:118-129) */
+      else if (l3 == CGPU_L3_IPV4)
         ph = or_pseudo_v4(rd32(p + l3_off + 12), rd32(p + l3_off + 16), (uint16_t)span, pr);
       else
         ph = or_pseudo_v6(p + l3_off + 8, p + l3_off + 24, (uint16_t)span, pr);
@@ -347,7 +365,8 @@ static void parse_one(const uint8_t *p, uint32_t len, uint32_t flags, uint32_t *
       if (l4 == CGPU_L4_UDP && l4_c == 0) l4_c = 0xFFFF; /* set_checksum udp.rs:137-140 */
       if (l4_c == r.l4_checksum) meta |= CGPU_META_L4_CSUM_OK;
     }
-    if (flags & CGPU_F_FLOW_HASH) /* Udp::flow udp.rs:151-159, Tcp::flow tcp.rs:409-417 */
+    /* Udp::flow udp.rs:151-159, Tcp::flow tcp.rs:409-417; ICMP has no flow */
+    if ((flags & CGPU_F_FLOW_HASH) && l4 != CGPU_L4_ICMP)
       hash = or_flow_hash(l3 == CGPU_L3_IPV6, r.src_ip, r.dst_ip, r.src_port, r.dst_port, pr);
   }
   meta |= (uint32_t)st;
@@ -360,7 +379,10 @@ static void parse_one(const uint8_t *p, uint32_t len, uint32_t flags, uint32_t *
 void or_parse_batch(const uint8_t *arena, const uint32_t *off, const uint16_t *len, uint32_t n,
                     uint32_t flags, uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
                     cgpu_hdr_record *fields) {
-  if ((flags & CGPU_F_ACCEPT_ALL) == 0) flags |= CGPU_F_ACCEPT_ALL;
+  /* no L3 (L4) type named: every IP version (UDP and TCP) accepted */
+  if ((flags & (CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6)) == 0) flags |= CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6;
+  if ((flags & (CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP | CGPU_F_ACCEPT_ICMP)) == 0)
+    flags |= CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP;
   for (uint32_t i = 0; i < n; ++i)
     parse_one(arena + off[i], len[i], flags, meta + i,
               (flags & (CGPU_F_CSUM_IP | CGPU_F_CSUM_L4)) && csum ? csum + i : NULL,

@@ -116,6 +116,24 @@ KATS = [
      "expect": {"ip_csum": 0x9997}},
     {"packet": "ICMPV4_PACKET", "src": "SURVEY.md Appendix B (icmp/v4/mod.rs:469 fixture)",
      "parse": "v4", "expect": {"ip_csum": 0x2B73}},
+    # ICMP (typed parse Ipv4 -> Icmpv4 / Ipv6 -> Icmpv6<Ipv6>). src_port /
+    # dst_port of the record carry msg_type / code for ICMP (capsule_gpu.h).
+    {"packet": "ICMPV4_PACKET", "src": "core/src/packets/icmp/v4/mod.rs:459-470",
+     "parse": "icmp", "expect": {"l4": "ICMP", "msg_type": 8, "code": 0,
+                                 "l4_checksum": 0x2A5C}},
+    {"packet": "ICMPV4_PACKET", "src": "core/src/packets/icmp/v4/mod.rs:503-514",
+     "parse": "icmp", "expect": {"l4_csum": 0x2A5C}},
+    {"packet": "IPV4_UDP_PACKET", "src": "core/src/packets/icmp/v4/mod.rs:494-501",
+     "parse": "icmp", "status": "NOT_ICMPV4"},
+    {"packet": "ROUTER_ADVERT_PACKET", "src": "core/src/packets/icmp/v6/mod.rs:513-524",
+     "parse": "icmp", "expect": {"l4": "ICMP", "msg_type": 134, "code": 0,
+                                 "l4_checksum": 0xF50C}},
+    {"packet": "ROUTER_ADVERT_PACKET", "src": "core/src/packets/icmp/v6/mod.rs:559-571",
+     "parse": "icmp", "expect": {"l4_csum": 0xF50C}},
+    {"packet": "ICMPV6_PACKET", "src": "core/src/packets/icmp/v6/mod.rs:541-548",
+     "parse": "icmp", "expect": {"l4": "ICMP"}},
+    {"packet": "IPV6_TCP_PACKET", "src": "core/src/packets/icmp/v6/mod.rs:550-557",
+     "parse": "icmp", "status": "NOT_ICMPV6"},
 ]
 
 # checksum.rs:226-229

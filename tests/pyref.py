@@ -2,14 +2,16 @@
 plain Python (test infrastructure only), used to cross-check the C oracle on
 small batches so the oracle is not trusted on its own say-so.
 
-Follows core/src/packets/{ethernet,ip/v4,ip/v6/mod,udp,tcp,checksum}.rs and
+Follows core/src/packets/{ethernet,ip/v4,ip/v6/mod,udp,tcp,checksum}.rs,
+icmp/v4/mod.rs:118-129,205-220, icmp/v6/mod.rs:123-138,217-232 and
 core/src/dpdk/mbuf.rs:313-327; the flow hash uses hashlib-free SipHash-1-3.
 """
 import struct
 
 ST = {"OK": 0, "ETH_BAD_OFFSET": 1, "ETH_OUT_OF_BUFFER": 2, "NOT_IPV4": 3, "NOT_IPV6": 4,
       "NOT_IP": 5, "L3_BAD_OFFSET": 6, "L3_OUT_OF_BUFFER": 7, "NOT_UDP": 8, "NOT_TCP": 9,
-      "NOT_L4": 10, "L4_BAD_OFFSET": 11, "L4_OUT_OF_BUFFER": 12}
+      "NOT_L4": 10, "L4_BAD_OFFSET": 11, "L4_OUT_OF_BUFFER": 12, "NOT_ICMPV4": 15,
+      "NOT_ICMPV6": 16}
 M64 = (1 << 64) - 1
 
 
@@ -70,8 +72,11 @@ def flow_bytes(v6, src, dst, sport, dport, proto):
 def parse(p, flags):
     """-> (status, meta_without_status, ip_c, l4_c, hash)"""
     acc4, acc6, accu, acct = (flags >> 0) & 1, (flags >> 1) & 1, (flags >> 2) & 1, (flags >> 3) & 1
-    if not flags & 0xF:
-        acc4 = acc6 = accu = acct = 1
+    acci = (flags >> 7) & 1
+    if not flags & 0x3:
+        acc4 = acc6 = 1
+    if not (accu or acct or acci):
+        accu = acct = 1
     n = len(p)
     meta, ip_c, l4_c, h = 0, 0, 0, 0
     if n == 0:
@@ -109,31 +114,38 @@ def parse(p, flags):
     else:
         proto = ip[6]
         src, dst = ip[8:24], ip[24:40]
+    icmp_proto = 1 if l3 == 1 else 58
     if accu and proto == 17:
         l4, l4len, cs = 1, 8, 6
     elif acct and proto == 6:
         l4, l4len, cs = 2, 20, 16
+    elif acci and proto == icmp_proto:
+        l4, l4len, cs = 3, 4, 2
+    elif accu + acct + acci > 1:
+        return ST["NOT_L4"], meta, ip_c, l4_c, h
     else:
-        return (ST["NOT_L4"] if accu and acct else ST["NOT_UDP"] if accu else ST["NOT_TCP"],
-                meta, ip_c, l4_c, h)
+        return (ST["NOT_UDP"] if accu else ST["NOT_TCP"] if acct else
+                ST["NOT_ICMPV4"] if l3 == 1 else ST["NOT_ICMPV6"], meta, ip_c, l4_c, h)
     o = hl + l3len
     if not o < n:
         return ST["L4_BAD_OFFSET"], meta, ip_c, l4_c, h
     if o + l4len > n:
         return ST["L4_OUT_OF_BUFFER"], meta, ip_c, l4_c, h
     meta |= l4 << 18
-    pr = 17 if l4 == 1 else 6
+    pr = {1: 17, 2: 6, 3: icmp_proto}[l4]
     if flags & 0x20:
         span = bytearray(p[o:]); span[cs:cs + 2] = b"\0\0"
         segs = sum(struct.unpack(">%dH" % (len(src) // 2), src)) + \
             sum(struct.unpack(">%dH" % (len(dst) // 2), dst))
         ph = fold(segs + pr + len(span))
+        if l4 == 3 and l3 == 1:
+            ph = 0  # Icmpv4::compute_checksum: compute(0, data)
         l4_c = compute(ph, bytes(span))
         if l4 == 1 and l4_c == 0:
             l4_c = 0xFFFF
         if l4_c == ((p[o + cs] << 8) | p[o + cs + 1]):
             meta |= 1 << 21
-    if flags & 0x40:
+    if flags & 0x40 and l4 != 3:  # ICMP has no Flow
         sport, dport = (p[o] << 8) | p[o + 1], (p[o + 2] << 8) | p[o + 3]
         h = siphash13(flow_bytes(l3 == 2, bytes(src), bytes(dst), sport, dport, pr))
     return 0, meta, ip_c, l4_c, h

@@ -14,7 +14,8 @@ ALL = N.F_ACCEPT_ALL | N.F_CSUM_IP | N.F_CSUM_L4 | N.F_FLOW_HASH
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_fuzz_oracle_vs_pyref(seed):
     arena, off, ln = synth.fuzz(300, seed=seed)
-    for flags in (ALL, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_L4, N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | 0x70):
+    for flags in (ALL, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_L4, N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | 0x70,
+                  ALL | N.F_ACCEPT_ICMP, N.F_ACCEPT_ICMP | 0x70, N.F_ACCEPT_V4 | N.F_ACCEPT_ICMP | 0x70):
         meta, csum, h, _ = oracle_lib.parse_batch(arena, off, ln, flags, fields=False)
         for i in range(len(off)):
             fr = bytes(arena[off[i] : off[i] + ln[i]])
@@ -27,11 +28,13 @@ def test_fuzz_oracle_vs_pyref(seed):
 def test_fuzz_covers_every_status():
     arena, off, ln = synth.fuzz(2000, seed=7)
     seen = set()
-    for flags in (ALL, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | 0x70, N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | 0x70):
+    for flags in (ALL, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | 0x70, N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | 0x70,
+                  N.F_ACCEPT_ICMP | 0x70):
         meta, _, _, _ = oracle_lib.parse_batch(arena, off, ln, flags, fields=False)
         seen |= set((meta & 0xFF).tolist())
     for s in ("OK", "ETH_BAD_OFFSET", "ETH_OUT_OF_BUFFER", "NOT_IPV4", "NOT_IPV6", "NOT_IP",
-              "L3_OUT_OF_BUFFER", "NOT_UDP", "NOT_TCP", "NOT_L4", "L4_OUT_OF_BUFFER"):
+              "L3_OUT_OF_BUFFER", "NOT_UDP", "NOT_TCP", "NOT_L4", "L4_OUT_OF_BUFFER",
+              "NOT_ICMPV4", "NOT_ICMPV6"):
         assert N.PKT[s] in seen, s
 
 

@@ -27,6 +27,7 @@ PARSE_FLAGS = {  # which typed parse the reference test performed
     "v6": N.F_ACCEPT_V6 | N.F_ACCEPT_UDP | N.F_ACCEPT_TCP,
     "udp": N.F_ACCEPT_V4 | N.F_ACCEPT_V6 | N.F_ACCEPT_UDP,
     "tcp": N.F_ACCEPT_V4 | N.F_ACCEPT_V6 | N.F_ACCEPT_TCP,
+    "icmp": N.F_ACCEPT_V4 | N.F_ACCEPT_V6 | N.F_ACCEPT_ICMP | N.F_CSUM_L4,
 }
 
 
@@ -52,6 +53,12 @@ def test_reference_kat(kat):
             got = (int(r["ip_flags"]) >> 1) & 1
         elif key in ("udp_length", "window"):
             got = int(r["udp_length_or_window"])
+        elif key == "msg_type":
+            got = int(r["src_port"])
+        elif key == "code":
+            got = int(r["dst_port"])
+        elif key == "l4":
+            got = ["NONE", "UDP", "TCP", "ICMP"][N.meta_l4(meta)]
         elif key == "ip_csum":
             got = csum & 0xFFFF
         elif key == "l4_csum":

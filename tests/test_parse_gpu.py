@@ -59,7 +59,7 @@ def test_reference_fixtures_every_flag_combination(ctx):
     for v in pk.values():
         frames += [bytes.fromhex(h) for h in v.get("packets", [])]
     arena, off, ln = synth.pack_frames(frames)
-    for acc in range(16):
+    for acc in list(range(16)) + [a | N.F_ACCEPT_ICMP for a in range(16)]:
         for feat in (0, N.F_CSUM_IP, N.F_CSUM_L4, N.F_FLOW_HASH, 0x70):
             assert_parity(ctx, arena, off, ln, acc | feat, fields=True)
     assert_parity(ctx, arena, off, ln, ALL, fields=False)
@@ -69,7 +69,8 @@ def test_reference_fixtures_every_flag_combination(ctx):
 def test_fuzz_unaligned_edge_cases(ctx, seed):
     arena, off, ln = synth.fuzz(3000, seed=seed)
     for flags in (ALL, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_L4,
-                  N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | N.F_FLOW_HASH, N.F_CSUM_IP | N.F_CSUM_L4):
+                  N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | N.F_FLOW_HASH, N.F_CSUM_IP | N.F_CSUM_L4,
+                  ALL | N.F_ACCEPT_ICMP, N.F_ACCEPT_ICMP | N.F_CSUM_L4 | N.F_CSUM_IP):
         assert_parity(ctx, arena, off, ln, flags, fields=True)
     assert_parity(ctx, arena, off, ln, ALL, fields=False)
 
@@ -80,7 +81,8 @@ def test_every_length_boundary(ctx):
     edge at 96 B, the streamed tail, odd spans)."""
     rng = np.random.default_rng(9)
     frames = []
-    for kind in (synth.V4_UDP, synth.V4_TCP, synth.V6_UDP, synth.V6_TCP):
+    for kind in (synth.V4_UDP, synth.V4_TCP, synth.V6_UDP, synth.V6_TCP, synth.V4_ICMP,
+                 synth.V6_ICMP):
         for vlan in (0, 1, 2):
             full = bytes(synth.build_frames(rng, 1, kind, 180, vlan)[0])
             frames += [full[:L] for L in range(0, 181)]
@@ -91,6 +93,7 @@ def test_every_length_boundary(ctx):
         arena, off, ln = synth.pack_frames(frames)
         arena = np.concatenate([np.zeros(shift, np.uint8), arena])
         assert_parity(ctx, arena, off + shift, ln, ALL)
+        assert_parity(ctx, arena, off + shift, ln, ALL | N.F_ACCEPT_ICMP)
 
 
 def test_packet_flush_with_arena_end(ctx):
