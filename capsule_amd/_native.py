@@ -22,6 +22,7 @@ PKT_STATUS = [
     "OK", "ETH_BAD_OFFSET", "ETH_OUT_OF_BUFFER", "NOT_IPV4", "NOT_IPV6", "NOT_IP",
     "L3_BAD_OFFSET", "L3_OUT_OF_BUFFER", "NOT_UDP", "NOT_TCP", "NOT_L4", "L4_BAD_OFFSET",
     "L4_OUT_OF_BUFFER", "NOT_RESIZED", "TABLE_FULL", "NOT_ICMPV4", "NOT_ICMPV6",
+    "EXT_BAD_OFFSET", "EXT_OUT_OF_BUFFER", "SRH_INCONSISTENT",
 ]
 PKT = {name: i for i, name in enumerate(PKT_STATUS)}
 
@@ -41,6 +42,8 @@ F_CSUM_IP = 1 << 4
 F_CSUM_L4 = 1 << 5
 F_FLOW_HASH = 1 << 6
 F_ACCEPT_ICMP = 1 << 7  # not part of F_ACCEPT_ALL
+F_V6_EXT = 1 << 8       # IPv6 SegmentRouting / Fragment headers before L4
+EXT_NONE, EXT_SRH, EXT_FRAGMENT = 0, 1, 2
 
 ACT, DROP, ABORT = 0, 1, 2
 
@@ -84,6 +87,7 @@ class ParseOut(ctypes.Structure):
         ("csum", ctypes.c_void_p),
         ("flow_hash", ctypes.c_void_p),
         ("fields", ctypes.c_void_p),
+        ("ext", ctypes.c_void_p),
     ]
 
 
@@ -100,6 +104,14 @@ HDR_RECORD_FIELDS = [
     ("pad3", "<u2"),
 ]
 HDR_RECORD_SIZE = 96
+
+EXT_RECORD_FIELDS = [  # cgpu_ext_record, 48 bytes
+    ("kind", "u1"), ("next_header", "u1"), ("header_len", "<u2"), ("hdr_ext_len", "u1"),
+    ("routing_type", "u1"), ("segments_left", "u1"), ("last_entry", "u1"), ("srh_flags", "u1"),
+    ("more_fragments", "u1"), ("tag", "<u2"), ("fragment_offset", "<u2"), ("pad0", "<u2"),
+    ("identification", "<u4"), ("pad1", "<u4"), ("segment0", "u1", (16,)), ("pad2", "u1", (8,)),
+]
+EXT_RECORD_SIZE = 48
 
 # Every symbol include/capsule_gpu.h declares (checked by tests/test_abi.py).
 EXPORTS = [

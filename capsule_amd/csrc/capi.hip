@@ -99,6 +99,9 @@ const char *cgpu_pkt_status_str(int s) {
     case CGPU_PKT_NOT_L4: return "not a packet of an accepted L4 type.";
     case CGPU_PKT_NOT_ICMPV4: return "not an ICMPv4 packet.";
     case CGPU_PKT_NOT_ICMPV6: return "not an ICMPv6 packet.";
+    case CGPU_PKT_EXT_BAD_OFFSET: return "IPv6 extension: bad offset";
+    case CGPU_PKT_EXT_OUT_OF_BUFFER: return "IPv6 extension: out of buffer";
+    case CGPU_PKT_SRH_INCONSISTENT: return "Packet has inconsistent segment list length.";
     case CGPU_PKT_L4_BAD_OFFSET: return "L4: bad offset";
     case CGPU_PKT_L4_OUT_OF_BUFFER: return "L4: out of buffer";
     case CGPU_PKT_NOT_RESIZED: return "buffer not resized";
@@ -164,11 +167,12 @@ int cgpu_parse_batch(cgpu_ctx *ctx, const cgpu_batch *batch, uint32_t flags,
   a.off = batch->off;
   a.len = batch->len;
   a.n = batch->n;
-  a.accept = flags & (CGPU_F_ACCEPT_ALL | CGPU_F_ACCEPT_ICMP);
+  a.accept = flags & (CGPU_F_ACCEPT_ALL | CGPU_F_ACCEPT_ICMP | CGPU_F_V6_EXT);
   a.meta = out->meta;
   a.csum = out->csum;
   a.hash = out->flow_hash;
   a.fields = out->fields;
+  a.ext = out->ext;
   hipError_t e = cgpu::launch_parse(a, flags, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e);
   return ok();
@@ -228,6 +232,7 @@ static int parse_and_return(cgpu_ctx *ctx, const uint8_t *arena, size_t arena_le
   o.csum = (uint32_t *)(ctx->d_desc + lay.csum);
   o.flow_hash = (uint64_t *)(ctx->d_desc + lay.hash);
   o.fields = fields ? (cgpu_hdr_record *)(ctx->d_desc + lay.fields) : nullptr;
+  o.ext = nullptr;
   if (!csum) flags &= ~(CGPU_F_CSUM_IP | CGPU_F_CSUM_L4);
   if (!flow_hash) flags &= ~CGPU_F_FLOW_HASH;
   if (int e = cgpu_parse_batch(ctx, &b, flags, &o, s)) return e;

@@ -41,6 +41,14 @@ __device__ __forceinline__ uint32_t load4_tail(rsrc_t rs, uint32_t byte_off, uin
   return v;
 }
 
+// The dword at any arena byte offset (tail-safe: zero past the arena end).
+__device__ __forceinline__ uint32_t load4_any(rsrc_t rs, uint32_t byte_off, uint32_t arena_len) {
+  const uint32_t sh = byte_off & 3u, b = byte_off - sh;
+  const uint32_t lo = load4_tail(rs, b, arena_len);
+  const uint32_t hi = sh ? load4_tail(rs, b + 4u, arena_len) : 0u;
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
 // 16 bytes at a 4-byte-aligned arena offset.  Near the end of the arena the
 // load is split so that bytes up to the last one are still returned (and
 // zeros past it).

@@ -17,11 +17,12 @@ struct ParseArgs {
   const uint32_t *off;
   const uint16_t *len;
   uint32_t n;
-  uint32_t accept;  // CGPU_F_ACCEPT_* bits
+  uint32_t accept;  // CGPU_F_ACCEPT_* bits and CGPU_F_V6_EXT
   uint32_t *meta;
   uint32_t *csum;
   uint64_t *hash;
   cgpu_hdr_record *fields;
+  cgpu_ext_record *ext;  // optional, with CGPU_F_V6_EXT
 };
 
 hipError_t launch_parse(const ParseArgs &a, uint32_t flags, hipStream_t s);

@@ -28,6 +28,8 @@
 //   Icmpv4/Icmpv6::try_parse   core/src/packets/icmp/v4/mod.rs:205-220, icmp/v6/mod.rs:217-232 (4 B)
 //   Icmpv4::compute_checksum   icmp/v4/mod.rs:118-129 (no pseudo-header)
 //   Icmpv6::compute_checksum   icmp/v6/mod.rs:123-138 (pseudo-header, protocol 58)
+//   SegmentRouting::try_parse  core/src/packets/ip/v6/srh.rs:299-327, dst()/pseudo_header :421-470
+//   Fragment::try_parse        core/src/packets/ip/v6/fragment.rs:187-202
 #include "capsule_gpu.h"
 #include "device_common.hpp"
 #include "kernels.hpp"
@@ -183,12 +185,58 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   const bool v4 = ether_type == 0x0800u && (a.accept & CGPU_F_ACCEPT_V4);
   const bool v6 = ether_type == 0x86ddu && (a.accept & CGPU_F_ACCEPT_V6);
   const uint32_t l3_len = v6 ? 40u : 20u;
-  const uint32_t proto = v6 ? (Q[5] & 0xffu) : (Q[5] >> 24);
+  const uint32_t proto0 = v6 ? (Q[5] & 0xffu) : (Q[5] >> 24);
+  // --- IPv6 extension header (CGPU_F_V6_EXT): SegmentRouting (43) or
+  // Fragment (44) behind IPv6, read per lane from memory (rare: the L4
+  // header behind it can lie past the register window) -------------------
+  const bool xcand = (a.accept & CGPU_F_V6_EXT) && v6 && len > eth_len && eth_len + 40u <= len &&
+                     (proto0 == 43u || proto0 == 44u);
+  uint32_t proto = proto0, l4_off = eth_len + l3_len;
+  uint32_t xkind = 0u, xst = 0u, xhl = 0u, X0 = 0u, X1 = 0u;
+  uint32_t S0[4] = {0u, 0u, 0u, 0u};  // segments[0], LE dwords of its wire bytes
+  uint32_t XU[5] = {0u, 0u, 0u, 0u, 0u};
+  bool xok = false;  // the extension parsed: L4 sits at l4_off behind it
+  if (__ballot(xcand)) {
+    if (xcand) {
+      const uint32_t xo = eth_len + 40u;  // the IPv6 payload offset
+      xkind = proto0 == 43u ? CGPU_EXT_SRH : CGPU_EXT_FRAGMENT;
+      if (xo >= len) {
+        xst = CGPU_PKT_EXT_BAD_OFFSET;  // read_data(offset) (mbuf.rs:313-327)
+      } else if (xo + 8u > len) {
+        xst = CGPU_PKT_EXT_OUT_OF_BUFFER;
+      } else {
+        X0 = load4_any(rs, off + xo, a.arena_len);
+        X1 = load4_any(rs, off + xo + 4u, a.arena_len);
+        if (xkind == CGPU_EXT_SRH) {
+          const uint32_t hel = (X0 >> 8) & 0xffu, nseg = (X1 & 0xffu) + 1u;
+          if (!(hel != 0u && 2u * nseg == hel)) {
+            xst = CGPU_PKT_SRH_INCONSISTENT;
+          } else if (xo + 8u >= len) {  // read_data_slice(offset + 8, segments) (mbuf.rs:365-380)
+            xst = CGPU_PKT_EXT_BAD_OFFSET;
+          } else if (xo + 8u + 16u * nseg > len) {
+            xst = CGPU_PKT_EXT_OUT_OF_BUFFER;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) S0[j] = load4_any(rs, off + xo + 8u + 4u * j, a.arena_len);
+            xhl = 8u + 16u * nseg;
+          }
+        } else {
+          xhl = 8u;
+        }
+        if (xst == 0u) {
+          xok = true;
+          proto = X0 & 0xffu;  // next_header of the extension
+          l4_off = xo + xhl;
+#pragma unroll
+          for (int j = 0; j < 5; ++j) XU[j] = load4_any(rs, off + l4_off + 4u * j, a.arena_len);
+        }
+      }
+    }
+  }
   const bool udp = proto == 17u && (a.accept & CGPU_F_ACCEPT_UDP);
   const bool tcp = proto == 6u && (a.accept & CGPU_F_ACCEPT_TCP);
   // ProtocolNumbers::Icmpv4 (1) under IPv4, Icmpv6 (58) under IPv6 (ip/mod.rs:41-75)
   const bool icmp = proto == (v6 ? 58u : 1u) && (a.accept & CGPU_F_ACCEPT_ICMP);
-  const uint32_t l4_off = eth_len + l3_len;
   const uint32_t l4_len = udp ? 8u : (icmp ? 4u : 20u);
   uint32_t st = CGPU_PKT_OK;
   bool eth_ok = false, l3_ok = false;
@@ -207,7 +255,9 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       st = CGPU_PKT_L3_OUT_OF_BUFFER;
     } else {
       l3_ok = true;
-      if (!udp && !tcp && !icmp) {
+      if (xst != 0u) {
+        st = xst;
+      } else if (!udp && !tcp && !icmp) {
         // exactly one accepted L4 type: its own error; several: NOT_L4
         const uint32_t acc = a.accept & (CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP | CGPU_F_ACCEPT_ICMP);
         st = acc == CGPU_F_ACCEPT_UDP    ? CGPU_PKT_NOT_UDP
@@ -231,12 +281,13 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   }
   if (l3_ok) meta |= (v6 ? CGPU_L3_IPV6 : CGPU_L3_IPV4) << 16;
   if (l4_ok) meta |= (udp ? CGPU_L4_UDP : (icmp ? CGPU_L4_ICMP : CGPU_L4_TCP)) << 18;
+  if (xok) meta |= xkind << 24;
 
   // L4 header dwords (L4 starts at normalized byte 34 for v4, 54 for v6)
   uint32_t U[5];
 #pragma unroll
   for (int j = 0; j < 5; ++j)
-    U[j] = __builtin_amdgcn_alignbyte(v6 ? Q[14 + j] : Q[9 + j], v6 ? Q[13 + j] : Q[8 + j], 2);
+    U[j] = xok ? XU[j] : __builtin_amdgcn_alignbyte(v6 ? Q[14 + j] : Q[9 + j], v6 ? Q[13 + j] : Q[8 + j], 2);
 
   uint32_t ip_c = 0, l4_c = 0;
   if (IPC && l3_ok && !v6) {
@@ -273,6 +324,32 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     // addresses (bytes 26..33) back out of the exact sum
     if (icmp && !v6) s -= (Q[6] >> 16) + (Q[7] & 0xffffu) + (Q[7] >> 16) + (Q[8] & 0xffffu);
     has_tail = endn > kQEnd;  // span continues past the window
+    if (xok) {
+      // Behind an extension header: src + (segments[0] behind a routing
+      // header, else dst) + the span [l4_off, len) read from memory.  Sums mod
+      // 0xFFFF suffice here: the pseudo-header's length and protocol terms
+      // added at the end are positive (always IPv6).
+      uint32_t x = sad16(Q[5] & 0xffff0000u, 0u);  // src: normalized bytes 22..37
+      x = sad16(Q[6], x);
+      x = sad16(Q[7], x);
+      x = sad16(Q[8], x);
+      x = sad16(Q[9] & 0xffffu, x);
+      if (xkind == CGPU_EXT_SRH) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x = sad16(S0[j], x);
+      } else {  // dst: normalized bytes 38..53
+        x = sad16(Q[9] & 0xffff0000u, x);
+        x = sad16(Q[10], x);
+        x = sad16(Q[11], x);
+        x = sad16(Q[12], x);
+        x = sad16(Q[13] & 0xffffu, x);
+      }
+      uint32_t r = fold64(sum_abs(rs, a.arena_len, off + l4_off, off + len));
+      if (off & 1u) r = swap16(r);  // absolute parity -> packet parity (l4_off is even)
+      stored_le = udp ? (XU[1] >> 16) : (icmp ? (XU[0] >> 16) : (XU[4] & 0xffffu));
+      s = x + r + (0xffffu - stored_le);
+      has_tail = false;
+    }
   }
   // Hash and header record first: only the checksum state stays live across
   // the cooperative tail loop below (register pressure).
@@ -293,7 +370,11 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   if (HASH) {
     uint64_t h = 0;
     if (l4_ok && !icmp) {  // Udp::flow / Tcp::flow (udp.rs:151-159, tcp.rs:409-417); ICMP has none
-      h = flow_hash(v6, src, dst, be16_lo(U[0]), be16_hi(U[0]), udp ? 17u : 6u);
+      // behind a routing header the flow's dst is SegmentRouting::dst() = segments[0]
+      const bool sdst = xok && xkind == CGPU_EXT_SRH;
+      const uint32_t fdst[4] = {sdst ? S0[0] : dst[0], sdst ? S0[1] : dst[1], sdst ? S0[2] : dst[2],
+                                sdst ? S0[3] : dst[3]};
+      h = flow_hash(v6, src, fdst, be16_lo(U[0]), be16_hi(U[0]), udp ? 17u : 6u);
     }
     if (valid) a.hash[i] = h;
   }
@@ -354,6 +435,31 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       u32x4 v = {R[4 * q], R[4 * q + 1], R[4 * q + 2], R[4 * q + 3]};
       out[q] = v;
     }
+  }
+  if (a.ext != nullptr && valid) {  // the extension record (cgpu_ext_record, 48 B)
+    u32x4 e0 = {0u, 0u, 0u, 0u}, e1 = {0u, 0u, 0u, 0u}, e2 = {0u, 0u, 0u, 0u};
+    if (xok) {
+      const uint32_t nh = X0 & 0xffu;
+      if (xkind == CGPU_EXT_SRH) {  // srh.rs:499-507
+        e0[0] = xkind | (nh << 8) | (xhl << 16);
+        e0[1] = X0 >> 8 | ((X1 & 0xffu) << 24);  // hdr_ext_len, routing_type, segments_left, last_entry
+        e0[2] = ((X1 >> 8) & 0xffu) | (be16_hi(X1) << 16);  // flags, tag
+        e1[2] = S0[0];
+        e1[3] = S0[1];
+        e2[0] = S0[2];
+        e2[1] = S0[3];
+      } else {  // fragment.rs:322-327: frag_res_m = offset << 3 | M
+        const uint32_t frm = be16_hi(X0);
+        e0[0] = xkind | (nh << 8) | (xhl << 16);
+        e0[2] = (frm & 1u) << 8;
+        e0[3] = frm >> 3;
+        e1[0] = be32(X1);
+      }
+    }
+    u32x4 *out = reinterpret_cast<u32x4 *>(a.ext + i);
+    out[0] = e0;
+    out[1] = e1;
+    out[2] = e2;
   }
   if (L4C && __ballot(has_tail)) {
     // The tails of the wave's long frames (bytes past the register window) are

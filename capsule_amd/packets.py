@@ -112,8 +112,9 @@ class PacketBatch:
 class ParsedBatch:
     """SoA result of `parse`: meta, csum, flow_hash, fields (device tensors)."""
 
-    def __init__(self, meta, csum, flow_hash, fields):
+    def __init__(self, meta, csum, flow_hash, fields, ext=None):
         self.meta, self.csum, self.flow_hash, self.fields = meta, csum, flow_hash, fields
+        self.ext = ext  # [n, 48] uint8 extension records (CGPU_F_V6_EXT), or None
 
     def status(self):
         return self.meta & 0xFF
@@ -159,7 +160,9 @@ class ParseBuffers:
     csum=False: verify-only checksums (the CSUM_OK bits of meta are still
     set; the computed values are not stored)."""
 
-    def __init__(self, n, device, fields=False, csum=True):
+    def __init__(self, n, device, fields=False, csum=True, ext=False):
+        self.ext = (torch.empty((n, N.EXT_RECORD_SIZE), dtype=torch.uint8, device=device)
+                    if ext else None)
         self.meta = torch.empty(n, dtype=torch.int32, device=device)
         self.csum = torch.empty(n, dtype=torch.int32, device=device) if csum else None
         self.flow_hash = torch.empty(n, dtype=torch.int64, device=device)
@@ -167,31 +170,34 @@ class ParseBuffers:
                        if fields else None)
 
 
-def parse(ctx, batch, flags=None, fields=False, out=None, stream=None):
+def parse(ctx, batch, flags=None, fields=False, out=None, stream=None, ext=False):
     """Batched Ethernet -> Ipv4/Ipv6 -> Udp/Tcp parse + checksums + flow hash.
 
     Mirrors `parse::<Ethernet>()` (ethernet.rs:279) -> `parse::<Ipv4|Ipv6>()`
     (v4.rs:427, v6/mod.rs:274) -> `parse::<Udp|Tcp>()` (udp.rs:287, tcp.rs:558),
     plus `compute_checksum` evaluated on the bytes as they are and the hash of
     `flow()`.  Asynchronous on `stream` (torch's current stream by default).
+    ext=True (with N.F_V6_EXT in flags): also the IPv6 extension records.
     """
     if flags is None:
         flags = parse_flags()
     n = batch.n
     if out is None:
-        out = ParseBuffers(n, batch.arena.device, fields)
+        out = ParseBuffers(n, batch.arena.device, fields, ext=ext)
     po = N.ParseOut()
     po.meta = out.meta.data_ptr()
     po.csum = out.csum.data_ptr() if out.csum is not None else None
     po.flow_hash = out.flow_hash.data_ptr()
     po.fields = out.fields.data_ptr() if (fields and out.fields is not None) else None
+    po.ext = out.ext.data_ptr() if (ext and out.ext is not None) else None
     cb = batch.cbatch()
     rc = N.lib().cgpu_parse_batch(ctx.handle, ctypes.byref(cb), flags, ctypes.byref(po),
                                   _stream_handle(stream))
     N.check(rc, "cgpu_parse_batch")
     return ParsedBatch(out.meta[:n], out.csum[:n] if out.csum is not None else None,
                        out.flow_hash[:n],
-                       out.fields[:n] if (fields and out.fields is not None) else None)
+                       out.fields[:n] if (fields and out.fields is not None) else None,
+                       out.ext[:n] if (ext and out.ext is not None) else None)
 
 
 def parse_host(ctx, frames, flags=None, fields=False):

@@ -124,6 +124,65 @@ def build_frames(rng, m, kind, frame_len, vlan=0, hop_limit_min=0):
     return f
 
 
+def build_ext_frames(rng, m, l4, frame_len, ext, nseg=1, vlan=0):
+    """m reconciled IPv6 frames with one extension header before the L4 layer
+    (`l4` in UDP / TCP / ICMP6): ext "srh" = a routing header with `nseg`
+    random segments (srh.rs:499-507; hdr_ext_len = 2 nseg, random
+    segments_left < nseg, flags and tag), ext "frag" = a fragment header
+    (fragment.rs:322-327; random offset, M bit, identification).  The L4
+    checksum uses the pseudo-header of the extension's envelope: behind a
+    routing header dst = segments[0] (srh.rs:456-470)."""
+    eth_len = 14 + 4 * vlan
+    xl = 8 + 16 * nseg if ext == "srh" else 8
+    t = eth_len + 40 + xl
+    assert frame_len >= t + l4_header_len(l4), (frame_len, t)
+    f = rng.integers(0, 256, size=(m, frame_len), dtype=np.uint8)
+    if vlan == 0:
+        _put16(f, 12, ETH_IPV6)
+    elif vlan == 1:
+        _put16(f, 12, 0x8100)
+        _put16(f, 16, ETH_IPV6)
+    else:
+        _put16(f, 12, 0x88A8)
+        _put16(f, 16, 0x8100)
+        _put16(f, 20, ETH_IPV6)
+    o = eth_len
+    w = (np.uint64(6) << np.uint64(28)) | rng.integers(0, 1 << 28, m, dtype=np.uint64)
+    for b in range(4):
+        f[:, o + b] = ((w >> np.uint64(24 - 8 * b)) & np.uint64(0xFF)).astype(np.uint8)
+    _put16(f, o + 4, frame_len - o - 40)
+    x = o + 40
+    if ext == "srh":
+        f[:, o + 6] = 43
+        f[:, x] = l4
+        f[:, x + 1] = 2 * nseg
+        f[:, x + 2] = 4
+        f[:, x + 3] = rng.integers(0, nseg, m).astype(np.uint8)
+        f[:, x + 4] = nseg - 1
+        dst = f[:, x + 8: x + 24]
+    else:
+        f[:, o + 6] = 44
+        f[:, x] = l4
+        f[:, x + 1] = 0
+        dst = f[:, o + 24: o + 40]
+    if l4 == UDP:
+        _put16(f, t + 4, frame_len - t)
+        cs_at = t + 6
+    elif l4 == TCP:
+        cs_at = t + 16
+    else:
+        cs_at = t + 2
+    _put16(f, cs_at, 0)
+    span = frame_len - t
+    ph = _be_word_sum(f[:, o + 8: o + 24]) + _be_word_sum(np.ascontiguousarray(dst)) + \
+        np.uint64(l4 + span)
+    c = (~_fold(_fold(ph) + _be_word_sum(f[:, t:]))) & np.uint64(0xFFFF)
+    if l4 == UDP:
+        c = np.where(c == 0, np.uint64(0xFFFF), c)
+    _put16(f, cs_at, c)
+    return f
+
+
 def place(groups, order, slot=64):
     """Lay out frames of several same-length groups in `order` into an arena.
 

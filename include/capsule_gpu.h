@@ -68,7 +68,12 @@ enum cgpu_pkt_status {
   /* Icmpv4/Icmpv6::try_parse (icmp/v4/mod.rs:205-220, icmp/v6/mod.rs:217-232) */
   CGPU_PKT_NOT_ICMPV4 = 15,      /* "not an ICMPv4 packet."                  */
   CGPU_PKT_NOT_ICMPV6 = 16,      /* "not an ICMPv6 packet."                  */
-  CGPU_PKT_STATUS_COUNT = 17
+  /* SegmentRouting / Fragment::try_parse (ip/v6/srh.rs:299-327,
+   * ip/v6/fragment.rs:187-202), with CGPU_F_V6_EXT */
+  CGPU_PKT_EXT_BAD_OFFSET = 17,
+  CGPU_PKT_EXT_OUT_OF_BUFFER = 18,
+  CGPU_PKT_SRH_INCONSISTENT = 19, /* "Packet has inconsistent segment list length." */
+  CGPU_PKT_STATUS_COUNT = 20
 };
 
 /* ---- `meta` word layout (one u32 per packet) ---------------------------- */
@@ -80,6 +85,10 @@ enum cgpu_pkt_status {
 #define CGPU_META_L4_CSUM_OK (1u << 21)           /* stored == computed       */
 #define CGPU_META_DOT1Q (1u << 22)                /* Ethernet::is_dot1q       */
 #define CGPU_META_QINQ (1u << 23)                 /* Ethernet::is_qinq        */
+#define CGPU_META_EXT(m) (((m) >> 24) & 0x3u)     /* 0 none, 1 SRH, 2 Fragment */
+#define CGPU_EXT_NONE 0u
+#define CGPU_EXT_SRH 1u
+#define CGPU_EXT_FRAGMENT 2u
 #define CGPU_L3_NONE 0u
 #define CGPU_L3_IPV4 1u
 #define CGPU_L3_IPV6 2u
@@ -108,6 +117,15 @@ enum cgpu_pkt_status {
  * flow_hash is 0.  In the header record src_port = msg_type, dst_port =
  * code, l4_checksum = the stored checksum.  Not part of CGPU_F_ACCEPT_ALL. */
 #define CGPU_F_ACCEPT_ICMP (1u << 7)
+/* IPv6 extension headers: an IPv6 next header of 43 (Ipv6Route) is parsed
+ * as SegmentRouting<Ipv6> (srh.rs:299-327: fixed 8-B header, then
+ * hdr_ext_len == 2 * (last_entry + 1) != 0, then the segment list), 44
+ * (Ipv6Frag) as Fragment<Ipv6> (fragment.rs:187-202, 8 B); the L4 layer is
+ * then parsed behind it, on its next_header -- the dispatch a group_by on
+ * next_header would do.  One extension level.  Behind a routing header the
+ * pseudo-header and the flow use dst = segments[0] (srh.rs:421-470);
+ * behind a fragment header the IPv6 addresses.                            */
+#define CGPU_F_V6_EXT (1u << 8)
 
 /* ---- batch descriptor ---------------------------------------------------
  * A batch is an arena of packet bytes plus one (offset, data_len) pair per
@@ -160,6 +178,27 @@ typedef struct cgpu_hdr_record {
   uint16_t pad3;               /* 94                                       */
 } cgpu_hdr_record;
 
+/* The extension header of one packet (CGPU_F_V6_EXT), host byte order;
+ * zero when there is none or it did not parse.  48 bytes.                 */
+typedef struct cgpu_ext_record {
+  uint8_t kind;              /*  0 CGPU_EXT_*                               */
+  uint8_t next_header;       /*  1 SegmentRouting / Fragment::next_header   */
+  uint16_t header_len;       /*  2 8 + 16 * segments / 8                    */
+  uint8_t hdr_ext_len;       /*  4 SegmentRouting::hdr_ext_len             */
+  uint8_t routing_type;      /*  5 ::routing_type                          */
+  uint8_t segments_left;     /*  6 ::segments_left                         */
+  uint8_t last_entry;        /*  7 ::last_entry                            */
+  uint8_t srh_flags;         /*  8 ::flags                                 */
+  uint8_t more_fragments;    /*  9 Fragment::more_fragments                */
+  uint16_t tag;              /* 10 SegmentRouting::tag                     */
+  uint16_t fragment_offset;  /* 12 Fragment::fragment_offset               */
+  uint16_t pad0;             /* 14                                         */
+  uint32_t identification;   /* 16 Fragment::identification                */
+  uint32_t pad1;             /* 20                                         */
+  uint8_t segment0[16];      /* 24 SegmentRouting::segments()[0] (= dst()) */
+  uint8_t pad2[8];           /* 40                                         */
+} cgpu_ext_record;
+
 /* Outputs of cgpu_parse_batch, all device pointers with n entries.       */
 typedef struct cgpu_parse_out {
   uint32_t *meta;       /* required                                          */
@@ -167,6 +206,8 @@ typedef struct cgpu_parse_out {
                          * CSUM_OK bits of meta are set either way)          */
   uint64_t *flow_hash;  /* required with CGPU_F_FLOW_HASH                     */
   cgpu_hdr_record *fields; /* optional (NULL = skip field extraction)        */
+  cgpu_ext_record *ext;    /* optional (NULL = skip); all-zero records unless
+                           * CGPU_F_V6_EXT parsed an extension header       */
 } cgpu_parse_out;
 
 typedef struct cgpu_ctx cgpu_ctx;

@@ -216,7 +216,8 @@ static int eth_parse(const uint8_t *p, uint32_t data_len, eth_t *e) {
 
 /* ---- one packet through Ethernet -> Ipv4|Ipv6 -> Udp|Tcp ---------------- */
 static void parse_one(const uint8_t *p, uint32_t len, uint32_t flags, uint32_t *meta_out,
-                      uint32_t *csum_out, uint64_t *hash_out, cgpu_hdr_record *rec) {
+                      uint32_t *csum_out, uint64_t *hash_out, cgpu_hdr_record *rec,
+                      cgpu_ext_record *ext) {
   const int acc4 = (flags & CGPU_F_ACCEPT_V4) != 0, acc6 = (flags & CGPU_F_ACCEPT_V6) != 0;
   const int accu = (flags & CGPU_F_ACCEPT_UDP) != 0, acct = (flags & CGPU_F_ACCEPT_TCP) != 0;
   const int acci = (flags & CGPU_F_ACCEPT_ICMP) != 0;
@@ -224,6 +225,9 @@ static void parse_one(const uint8_t *p, uint32_t len, uint32_t flags, uint32_t *
   uint64_t hash = 0;
   cgpu_hdr_record r;
   memset(&r, 0, sizeof r);
+  cgpu_ext_record x;
+  memset(&x, 0, sizeof x);
+  const uint8_t *seg0 = NULL; /* SegmentRouting::dst() when behind a routing header */
 
   eth_t e;
   int st = eth_parse(p, len, &e);
@@ -294,12 +298,61 @@ static void parse_one(const uint8_t *p, uint32_t len, uint32_t flags, uint32_t *
     }
     meta |= (uint32_t)l3 << 16;
     l4_off = l3_off + l3_len;
+    /* CGPU_F_V6_EXT: SegmentRouting<Ipv6>::try_parse (ip/v6/srh.rs:299-327) or
+     * Fragment<Ipv6>::try_parse (ip/v6/fragment.rs:187-202), then L4 behind it */
+    if (l3 == CGPU_L3_IPV6 && (flags & CGPU_F_V6_EXT) && (proto == 43 || proto == 44)) {
+      const uint32_t xo = l4_off; /* envelope.payload_offset() */
+      uint32_t xhl = 0;
+      st = read_data(len, xo, 8, CGPU_PKT_EXT_BAD_OFFSET, CGPU_PKT_EXT_OUT_OF_BUFFER);
+      if (!st && proto == 43) {
+        const uint8_t *h = p + xo; /* SegmentRoutingHeader (srh.rs:499-507) */
+        const uint32_t hel = h[1], nseg = (uint32_t)h[4] + 1;
+        if (!(hel != 0 && 2 * nseg == hel)) {
+          st = CGPU_PKT_SRH_INCONSISTENT; /* "Packet has inconsistent segment list length." */
+        } else {
+          /* read_data_slice::<Ipv6Addr>(offset + 8, segments) (mbuf.rs:365-380) */
+          st = read_data(len, xo + 8, 16 * nseg, CGPU_PKT_EXT_BAD_OFFSET,
+                         CGPU_PKT_EXT_OUT_OF_BUFFER);
+        }
+        if (!st) {
+          xhl = 8 + 16 * nseg; /* header_len (srh.rs:274-276) */
+          seg0 = h + 8;
+          x.kind = CGPU_EXT_SRH;
+          x.hdr_ext_len = h[1];
+          x.routing_type = h[2];
+          x.segments_left = h[3];
+          x.last_entry = h[4];
+          x.srh_flags = h[5];
+          x.tag = rd16(h + 6);
+          memcpy(x.segment0, seg0, 16);
+        }
+      } else if (!st) {
+        const uint8_t *h = p + xo; /* FragmentHeader (fragment.rs:322-327) */
+        xhl = 8;
+        x.kind = CGPU_EXT_FRAGMENT;
+        x.fragment_offset = rd16(h + 2) >> 3; /* & FRAG_OS, >> 3 (:93-96) */
+        x.more_fragments = rd16(h + 2) & 1;   /* FLAG_MORE (:105-107) */
+        x.identification = rd32(h + 4);
+      }
+      if (!st) {
+        x.next_header = p[xo];
+        x.header_len = (uint16_t)xhl;
+        proto = p[xo]; /* next_protocol() of the extension */
+        l4_off = xo + xhl;
+        meta |= (uint32_t)x.kind << 24;
+      } else {
+        memset(&x, 0, sizeof x);
+        seg0 = NULL;
+      }
+    }
     /* Udp::try_parse (udp.rs:287-302) / Tcp::try_parse (tcp.rs:558-573) /
      * Icmpv4::try_parse (icmp/v4/mod.rs:205-220: protocol() == Icmpv4) /
      * Icmpv6::try_parse (icmp/v6/mod.rs:217-232: next_protocol() == Icmpv6) */
     uint32_t l4_len = 0;
     const uint8_t icmp_proto = l3 == CGPU_L3_IPV4 ? 0x01 : 0x3A; /* ip/mod.rs:41-75 */
-    if (accu && proto == 17) {
+    if (st) {
+      /* the extension header failed */
+    } else if (accu && proto == 17) {
       l4 = CGPU_L4_UDP;
       l4_len = 8;
     } else if (acct && proto == 6) {
@@ -358,8 +411,8 @@ static void parse_one(const uint8_t *p, uint32_t len, uint32_t flags, uint32_t *
         ph = 0; /* Icmpv4::compute_checksum: compute(0, data) (icmp/v4/mod.rs:118-129) */
       else if (l3 == CGPU_L3_IPV4)
         ph = or_pseudo_v4(rd32(p + l3_off + 12), rd32(p + l3_off + 16), (uint16_t)span, pr);
-      else
-        ph = or_pseudo_v6(p + l3_off + 8, p + l3_off + 24, (uint16_t)span, pr);
+      else /* behind a routing header: dst = segments[0] (srh.rs:456-470) */
+        ph = or_pseudo_v6(p + l3_off + 8, seg0 ? seg0 : p + l3_off + 24, (uint16_t)span, pr);
       l4_c = or_compute(ph, data, span);
       free(data);
       if (l4 == CGPU_L4_UDP && l4_c == 0) l4_c = 0xFFFF; /* set_checksum udp.rs:137-140 */
@@ -367,18 +420,20 @@ static void parse_one(const uint8_t *p, uint32_t len, uint32_t flags, uint32_t *
     }
     /* Udp::flow udp.rs:151-159, Tcp::flow tcp.rs:409-417; ICMP has no flow */
     if ((flags & CGPU_F_FLOW_HASH) && l4 != CGPU_L4_ICMP)
-      hash = or_flow_hash(l3 == CGPU_L3_IPV6, r.src_ip, r.dst_ip, r.src_port, r.dst_port, pr);
+      hash = or_flow_hash(l3 == CGPU_L3_IPV6, r.src_ip, seg0 ? seg0 : r.dst_ip, r.src_port,
+                          r.dst_port, pr);
   }
   meta |= (uint32_t)st;
   *meta_out = meta;
   if (csum_out) *csum_out = ip_c | (l4_c << 16);
   if (hash_out) *hash_out = hash;
   if (rec) *rec = r;
+  if (ext) *ext = x;
 }
 
-void or_parse_batch(const uint8_t *arena, const uint32_t *off, const uint16_t *len, uint32_t n,
-                    uint32_t flags, uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
-                    cgpu_hdr_record *fields) {
+void or_parse_batch_ext(const uint8_t *arena, const uint32_t *off, const uint16_t *len,
+                        uint32_t n, uint32_t flags, uint32_t *meta, uint32_t *csum,
+                        uint64_t *flow_hash, cgpu_hdr_record *fields, cgpu_ext_record *ext) {
   /* no L3 (L4) type named: every IP version (UDP and TCP) accepted */
   if ((flags & (CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6)) == 0) flags |= CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6;
   if ((flags & (CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP | CGPU_F_ACCEPT_ICMP)) == 0)
@@ -387,7 +442,13 @@ void or_parse_batch(const uint8_t *arena, const uint32_t *off, const uint16_t *l
     parse_one(arena + off[i], len[i], flags, meta + i,
               (flags & (CGPU_F_CSUM_IP | CGPU_F_CSUM_L4)) && csum ? csum + i : NULL,
               (flags & CGPU_F_FLOW_HASH) && flow_hash ? flow_hash + i : NULL,
-              fields ? fields + i : NULL);
+              fields ? fields + i : NULL, ext ? ext + i : NULL);
+}
+
+void or_parse_batch(const uint8_t *arena, const uint32_t *off, const uint16_t *len, uint32_t n,
+                    uint32_t flags, uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
+                    cgpu_hdr_record *fields) {
+  or_parse_batch_ext(arena, off, len, n, flags, meta, csum, flow_hash, fields, NULL);
 }
 
 /* bench/packets.rs:65-69 multi_parse_udp: parse::<Ethernet>() ->

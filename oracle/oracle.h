@@ -41,6 +41,10 @@ uint64_t or_flow_hash(int v6, const uint8_t *src, const uint8_t *dst, uint16_t s
                       uint16_t dst_port, uint8_t protocol);
 
 /* Batched parse with the cgpu_parse_batch output contract (host memory). */
+/* or_parse_batch plus the extension records (CGPU_F_V6_EXT); ext may be NULL */
+void or_parse_batch_ext(const uint8_t *arena, const uint32_t *off, const uint16_t *len,
+                        uint32_t n, uint32_t flags, uint32_t *meta, uint32_t *csum,
+                        uint64_t *flow_hash, cgpu_hdr_record *fields, cgpu_ext_record *ext);
 void or_parse_batch(const uint8_t *arena, const uint32_t *off, const uint16_t *len, uint32_t n,
                     uint32_t flags, uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
                     cgpu_hdr_record *fields);

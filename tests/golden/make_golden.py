@@ -134,6 +134,22 @@ KATS = [
      "parse": "icmp", "expect": {"l4": "ICMP"}},
     {"packet": "IPV6_TCP_PACKET", "src": "core/src/packets/icmp/v6/mod.rs:550-557",
      "parse": "icmp", "status": "NOT_ICMPV6"},
+    # IPv6 extension headers (CGPU_F_V6_EXT: dispatch on next_header 43 / 44)
+    {"packet": "SR_TCP_PACKET", "src": "core/src/packets/ip/v6/srh.rs:537-556",
+     "parse": "ext", "expect": {"ext.kind": 1, "ext.next_header": 6, "ext.hdr_ext_len": 6,
+                                "ext.routing_type": 4, "ext.segments_left": 0,
+                                "ext.last_entry": 2, "ext.tag": 0, "ext.header_len": 56,
+                                "ext.segment0": "20010db885a3000000008a2e03707333"}},
+    {"packet": "SR_TCP_PACKET", "src": "core/src/packets/ip/v6/srh.rs:684-698",
+     "parse": "ext", "expect": {"l4": "TCP", "src_port": 3464}},
+    {"packet": "IPV6_TCP_PACKET", "src": "core/src/packets/ip/v6/srh.rs:558-565",
+     "parse": "ext", "expect": {"ext.kind": 0, "l4": "TCP"}},
+    {"packet": "IPV6_FRAGMENT_PACKET", "src": "core/src/packets/ip/v6/fragment.rs:342-353",
+     "parse": "ext", "expect": {"ext.kind": 2, "ext.next_header": 17,
+                                "ext.fragment_offset": 543, "ext.more_fragments": 0,
+                                "ext.identification": 0xF88EB466, "ext.header_len": 8}},
+    {"packet": "IPV6_TCP_PACKET", "src": "core/src/packets/ip/v6/fragment.rs:355-362",
+     "parse": "ext", "expect": {"ext.kind": 0}},
 ]
 
 # checksum.rs:226-229

@@ -38,6 +38,8 @@ def load(name="liboracle.so"):
     L.or_flow_hash.argtypes = [i32, vp, vp, u16, u16, u8]
     L.or_parse_batch.restype = None
     L.or_parse_batch.argtypes = [vp, vp, vp, u32, u32, vp, vp, vp, vp]
+    L.or_parse_batch_ext.restype = None
+    L.or_parse_batch_ext.argtypes = [vp, vp, vp, u32, u32, vp, vp, vp, vp, vp]
     L.or_multi_parse_udp.restype = u32
     L.or_multi_parse_udp.argtypes = [vp, vp, vp, u32]
     L.or_portmap_new.restype = vp
@@ -69,6 +71,22 @@ def lib():
 
 def _p(a):
     return a.ctypes.data if a is not None else None
+
+
+def parse_batch_ext(arena, off, length, flags):
+    """Oracle parse with extension records -> (meta, csum, hash, fields [n,96], ext [n,48])."""
+    n = len(off)
+    arena = np.ascontiguousarray(arena, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    length = np.ascontiguousarray(length, np.uint16)
+    meta = np.zeros(n, np.uint32)
+    csum = np.zeros(n, np.uint32)
+    h = np.zeros(n, np.uint64)
+    fl = np.zeros((n, 96), np.uint8)
+    ext = np.zeros((n, 48), np.uint8)
+    lib().or_parse_batch_ext(_p(arena), _p(off), _p(length), n, flags, _p(meta), _p(csum), _p(h),
+                             _p(fl), _p(ext))
+    return meta, csum, h, fl, ext
 
 
 def parse_batch(arena, off, length, flags, fields=True):

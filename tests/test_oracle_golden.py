@@ -28,24 +28,34 @@ PARSE_FLAGS = {  # which typed parse the reference test performed
     "udp": N.F_ACCEPT_V4 | N.F_ACCEPT_V6 | N.F_ACCEPT_UDP,
     "tcp": N.F_ACCEPT_V4 | N.F_ACCEPT_V6 | N.F_ACCEPT_TCP,
     "icmp": N.F_ACCEPT_V4 | N.F_ACCEPT_V6 | N.F_ACCEPT_ICMP | N.F_CSUM_L4,
+    "ext": ALL | N.F_ACCEPT_ICMP | N.F_V6_EXT,
 }
+EXT = np.dtype(N.EXT_RECORD_FIELDS)
 
 
 def run_one(name, flags):
     fr = bytes.fromhex(PACKETS[name]["hex"])
     arena, off, ln = synth.pack_frames([fr])
-    meta, csum, h, fl = oracle_lib.parse_batch(arena, off, ln, flags)
-    return fr, int(meta[0]), int(csum[0]), int(h[0]), fl.view(REC).reshape(-1)[0]
+    meta, csum, h, fl, ext = oracle_lib.parse_batch_ext(arena, off, ln, flags)
+    return (fr, int(meta[0]), int(csum[0]), int(h[0]), fl.view(REC).reshape(-1)[0],
+            ext.view(EXT).reshape(-1)[0])
 
 
 @pytest.mark.parametrize("kat", KATS["kats"], ids=lambda k: f"{k['packet']}@{k['src']}")
 def test_reference_kat(kat):
-    fr, meta, csum, h, r = run_one(kat["packet"], PARSE_FLAGS[kat.get("parse")])
+    fr, meta, csum, h, r, x = run_one(kat["packet"], PARSE_FLAGS[kat.get("parse")])
     if "status" in kat:
         assert N.PKT_STATUS[meta & 0xFF] == kat["status"]
         return
     for key, want in kat.get("expect", {}).items():
-        if key in ("dst_mac", "src_mac", "src_ip", "dst_ip"):
+        if key == "ext.segment0":
+            got = bytes(x["segment0"]).hex()
+        elif key == "ext.kind":
+            got = int(x["kind"])
+            assert got == (meta >> 24) & 3
+        elif key.startswith("ext."):
+            got = int(x[key[4:]])
+        elif key in ("dst_mac", "src_mac", "src_ip", "dst_ip"):
             got = bytes(r[key]).hex()[: len(want)]
         elif key == "dont_fragment":
             got = int(r["ip_flags"]) & 1
@@ -140,7 +150,7 @@ def test_pcap_fixtures():
 def test_ipv6_tcp_fixture_has_wrong_stored_checksum():
     """IPV6_TCP_PACKET carries the v4 fixture's 0xa92c (byte_arrays.rs:155);
     the recomputed value is 0x1b1c."""
-    fr, meta, csum, h, r = run_one("IPV6_TCP_PACKET", ALL)
+    fr, meta, csum, h, r, _ = run_one("IPV6_TCP_PACKET", ALL)
     assert int(r["l4_checksum"]) == 0xA92C
     assert csum >> 16 == 0x1B1C
     assert not meta & N.META_L4_CSUM_OK

@@ -36,6 +36,27 @@ def gpu_parse(ctx, arena, off, ln, flags, fields=True):
     return meta, csum, h, fl
 
 
+def assert_ext_parity(ctx, arena, off, ln, flags):
+    """Every output including the extension records (CGPU_F_V6_EXT)."""
+    from capsule_amd import packets
+
+    b = packets.PacketBatch.from_numpy(arena, off, ln, DEV)
+    r = packets.parse(ctx, b, flags=flags, fields=True, ext=True)
+    torch.cuda.synchronize()
+    om, oc, oh, of, ox = oracle_lib.parse_batch_ext(arena, off, ln, flags)
+    gm = r.meta.cpu().numpy().view(np.uint32)
+    assert (gm == om).all(), ("meta", np.nonzero(gm != om)[0][:8], gm[gm != om][:4], om[gm != om][:4])
+    if flags & (N.F_CSUM_IP | N.F_CSUM_L4):  # outputs that were requested
+        gc = r.csum.cpu().numpy().view(np.uint32)
+        assert (gc == oc).all(), ("csum", np.nonzero(gc != oc)[0][:8])
+    if flags & N.F_FLOW_HASH:
+        gh = r.flow_hash.cpu().numpy().view(np.uint64)
+        assert (gh == oh).all(), ("hash", np.nonzero(gh != oh)[0][:8])
+    assert (r.fields.cpu().numpy() == of).all(), "fields"
+    gx = r.ext.cpu().numpy()
+    assert (gx == ox).all(), ("ext", np.nonzero((gx != ox).any(axis=1))[0][:8])
+
+
 def assert_parity(ctx, arena, off, ln, flags, fields=True):
     gm, gc, gh, gf = gpu_parse(ctx, arena, off, ln, flags, fields)
     om, oc, oh, of = oracle_lib.parse_batch(arena, off, ln, flags, fields)
@@ -196,3 +217,52 @@ def test_verify_only_mode_sets_same_meta(ctx):
     torch.cuda.synchronize()
     assert r2.csum is None
     assert torch.equal(r1.meta, r2.meta) and torch.equal(r1.flow_hash, r2.flow_hash)
+
+
+def ext_batch(seed):
+    """IPv6 routing (1..6 segments) and fragment headers before UDP / TCP /
+    ICMPv6, every VLAN depth, frames up to 1500 B, plus truncations at every
+    length of a few of them, inconsistent segment lists and plain frames."""
+    rng = np.random.default_rng(seed)
+    frames = []
+    for ext, nseg in [("srh", 1), ("srh", 2), ("srh", 3), ("srh", 6), ("frag", 1)]:
+        for l4 in (synth.UDP, synth.TCP, synth.ICMP6):
+            for vlan in (0, 1, 2):
+                need = 14 + 4 * vlan + 40 + (8 + 16 * nseg if ext == "srh" else 8) + \
+                    synth.l4_header_len(l4)
+                for L in (need, need + 1, need + 37, 300, 1500):
+                    frames.append(bytes(synth.build_ext_frames(rng, 1, l4, max(L, need), ext, nseg,
+                                                               vlan)[0]))
+    full = bytes(synth.build_ext_frames(rng, 1, synth.TCP, 220, "srh", 3, 1)[0])
+    frames += [full[:L] for L in range(0, 221)]
+    full = bytes(synth.build_ext_frames(rng, 1, synth.UDP, 120, "frag", 1, 0)[0])
+    frames += [full[:L] for L in range(0, 121)]
+    for _ in range(40):  # inconsistent segment lists (hdr_ext_len != 2 (last_entry + 1))
+        f = bytearray(synth.build_ext_frames(rng, 1, synth.TCP, 200, "srh", 2, 0)[0])
+        f[14 + 40 + int(rng.integers(1, 5, dtype=np.int64)) % 2 * 3 + 1] ^= 1 + int(rng.integers(0, 255))
+        frames.append(bytes(f))
+    a, o, l = synth.imix(300, seed=seed)
+    frames += [bytes(a[o[i]: o[i] + l[i]]) for i in range(len(o))]
+    order = rng.permutation(len(frames))
+    return [frames[i] for i in order]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_ipv6_extension_headers(ctx, seed):
+    frames = ext_batch(seed)
+    for shift in (0, 1, 2):
+        arena, off, ln = synth.pack_frames(frames)
+        arena = np.concatenate([np.zeros(shift, np.uint8), arena])
+        for flags in (ALL | N.F_V6_EXT | N.F_ACCEPT_ICMP, ALL | N.F_V6_EXT,
+                      N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | N.F_V6_EXT | N.F_CSUM_L4 | N.F_FLOW_HASH,
+                      ALL):
+            assert_ext_parity(ctx, arena, off + shift, ln, flags)
+
+
+def test_reference_fixtures_with_extensions(ctx):
+    pk = json.loads((GOLD / "reference_packets.json").read_text())
+    frames = [bytes.fromhex(v["hex"]) for v in pk.values() if "hex" in v]
+    arena, off, ln = synth.pack_frames(frames)
+    for acc in (N.F_ACCEPT_ALL, N.F_ACCEPT_V6 | N.F_ACCEPT_TCP, N.F_ACCEPT_V6 | N.F_ACCEPT_UDP):
+        for feat in (0, N.F_CSUM_L4, N.F_FLOW_HASH, 0x70, 0x70 | N.F_ACCEPT_ICMP):
+            assert_ext_parity(ctx, arena, off, ln, acc | feat | N.F_V6_EXT)
