@@ -110,7 +110,7 @@ __device__ __forceinline__ uint32_t chunk_excess(u32x4 v, uint32_t c, uint32_t f
   return e;
 }
 
-template <bool IPC, bool L4C, bool HASH, bool FIELDS>
+template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT>
 __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   // No early exit: lanes past n run with len 0 (status BadOffset) and store
@@ -189,14 +189,14 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   // --- IPv6 extension header (CGPU_F_V6_EXT): SegmentRouting (43) or
   // Fragment (44) behind IPv6, read per lane from memory (rare: the L4
   // header behind it can lie past the register window) -------------------
-  const bool xcand = (a.accept & CGPU_F_V6_EXT) && v6 && len > eth_len && eth_len + 40u <= len &&
+  const bool xcand = EXT && v6 && len > eth_len && eth_len + 40u <= len &&
                      (proto0 == 43u || proto0 == 44u);
   uint32_t proto = proto0, l4_off = eth_len + l3_len;
   uint32_t xkind = 0u, xst = 0u, xhl = 0u, X0 = 0u, X1 = 0u;
   uint32_t S0[4] = {0u, 0u, 0u, 0u};  // segments[0], LE dwords of its wire bytes
   uint32_t XU[5] = {0u, 0u, 0u, 0u, 0u};
   bool xok = false;  // the extension parsed: L4 sits at l4_off behind it
-  if (__ballot(xcand)) {
+  if (EXT && __ballot(xcand)) {
     if (xcand) {
       const uint32_t xo = eth_len + 40u;  // the IPv6 payload offset
       xkind = proto0 == 43u ? CGPU_EXT_SRH : CGPU_EXT_FRAGMENT;
@@ -542,21 +542,26 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
 
 }
 
-template <bool IPC, bool L4C, bool HASH, bool FIELDS>
+template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT>
 hipError_t launch_t(const ParseArgs &a, hipStream_t s) {
   const uint32_t grid = (a.n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS>), dim3(grid), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT>), dim3(grid), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
+template <bool IPC, bool L4C, bool HASH, bool FIELDS>
+hipError_t launch_e(const ParseArgs &a, bool ext, hipStream_t s) {
+  return ext ? launch_t<IPC, L4C, HASH, FIELDS, true>(a, s) : launch_t<IPC, L4C, HASH, FIELDS, false>(a, s);
+}
+
 template <bool IPC, bool L4C, bool HASH>
-hipError_t launch_f(const ParseArgs &a, bool fields, hipStream_t s) {
-  return fields ? launch_t<IPC, L4C, HASH, true>(a, s) : launch_t<IPC, L4C, HASH, false>(a, s);
+hipError_t launch_f(const ParseArgs &a, bool fields, bool ext, hipStream_t s) {
+  return fields ? launch_e<IPC, L4C, HASH, true>(a, ext, s) : launch_e<IPC, L4C, HASH, false>(a, ext, s);
 }
 
 template <bool IPC, bool L4C>
-hipError_t launch_h(const ParseArgs &a, bool hash, bool fields, hipStream_t s) {
-  return hash ? launch_f<IPC, L4C, true>(a, fields, s) : launch_f<IPC, L4C, false>(a, fields, s);
+hipError_t launch_h(const ParseArgs &a, bool hash, bool fields, bool ext, hipStream_t s) {
+  return hash ? launch_f<IPC, L4C, true>(a, fields, ext, s) : launch_f<IPC, L4C, false>(a, fields, ext, s);
 }
 
 }  // namespace
@@ -565,10 +570,11 @@ hipError_t launch_parse(const ParseArgs &a, uint32_t flags, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const bool ipc = flags & CGPU_F_CSUM_IP, l4c = flags & CGPU_F_CSUM_L4;
   const bool hash = flags & CGPU_F_FLOW_HASH, fields = a.fields != nullptr;
+  const bool ext = flags & CGPU_F_V6_EXT;  // the extension path is compiled out otherwise
   if (ipc) {
-    return l4c ? launch_h<true, true>(a, hash, fields, s) : launch_h<true, false>(a, hash, fields, s);
+    return l4c ? launch_h<true, true>(a, hash, fields, ext, s) : launch_h<true, false>(a, hash, fields, ext, s);
   }
-  return l4c ? launch_h<false, true>(a, hash, fields, s) : launch_h<false, false>(a, hash, fields, s);
+  return l4c ? launch_h<false, true>(a, hash, fields, ext, s) : launch_h<false, false>(a, hash, fields, ext, s);
 }
 
 }  // namespace cgpu
