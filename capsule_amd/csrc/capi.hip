@@ -58,7 +58,7 @@ struct cgpu_portmap {
   void *mem;
   // per-call scratch
   uint32_t *pkt_slot = nullptr;
-  uint32_t *block_sums = nullptr;
+  uint64_t *lookback = nullptr;
   void *rec_h = nullptr;  // deferred frames' header records
   void *rec_b = nullptr;
   uint32_t *defer = nullptr;
@@ -507,12 +507,14 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
     const size_t nb = cgpu::nat64_num_blocks(in->n) + 1;
     void *m = nullptr;
     const size_t o_sums = align_up(4ull * in->n, 256);
-    const size_t o_rech = o_sums + align_up(4ull * nb, 256);
+    const size_t o_rech = o_sums + align_up(8ull * nb, 256);
     const size_t o_recb = o_rech + align_up(16ull * in->n, 256);
     const size_t o_defer = o_recb + align_up(8ull * in->n, 256);
     if (hipMalloc(&m, o_defer + 4ull * in->n + 256) != hipSuccess) return fail(CGPU_ENOMEM);
     pm->pkt_slot = (uint32_t *)m;
-    pm->block_sums = (uint32_t *)((uint8_t *)m + o_sums);
+    pm->lookback = (uint64_t *)((uint8_t *)m + o_sums);
+    // status 0 = "not published" in every epoch
+    if (hipMemset(pm->lookback, 0, 8ull * nb) != hipSuccess) return fail(CGPU_EIO);
     pm->rec_h = (uint8_t *)m + o_rech;
     pm->rec_b = (uint8_t *)m + o_recb;
     pm->defer = (uint32_t *)((uint8_t *)m + o_defer);
@@ -531,7 +533,8 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   a.disposition = disposition;
   a.status = status;
   a.pkt_slot = pm->pkt_slot;
-  a.block_sums = pm->block_sums;
+  a.lookback = pm->lookback;
+  a.epoch = pm->calls;
   a.rec_h = (cgpu::u32x4 *)pm->rec_h;
   a.rec_b = (uint2 *)pm->rec_b;
   a.defer = pm->defer;

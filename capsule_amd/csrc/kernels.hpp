@@ -48,7 +48,7 @@ struct PortSlot {
 struct PortMapDev {
   PortSlot *slots;  // [cap]
   uint64_t *rev;    // [65536]: (first ordinal << 32 | slot), ~0 = none (ADDR_MAP, main.rs:38)
-  uint32_t *state;  // [6]: next_port, entries, batch_base, batch_new, deferred[2]
+  uint32_t *state;  // [9]: next_port, entries, -, -, deferred[2], chunk tickets[2], batch new keys
   uint32_t cap_mask;
 };
 
@@ -65,7 +65,8 @@ struct Nat64Args {
   uint8_t *disposition;
   uint8_t *status;
   uint32_t *pkt_slot;    // scratch [n]: table slot (or 0xffffffff)
-  uint32_t *block_sums;  // scratch [nblocks + 1]
+  uint64_t *lookback;    // scratch [nblocks]: K2's decoupled look-back words
+  uint32_t epoch;        // 6to4 call number (look-back words of other calls are stale)
   u32x4 *rec_h;          // scratch [n]: deferred 6to4 frames' IPv4 header dwords 0..3
   uint2 *rec_b;          // scratch [n]: header dword 4, VLAN depth
   uint32_t *defer;       // scratch [n]: indices of the deferred 6to4 frames

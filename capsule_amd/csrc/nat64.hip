@@ -30,12 +30,13 @@
 // A 6to4 frame whose key is not yet committed (first seen in this batch)
 // needs the batch-wide first-seen order, so the fused kernel defers it: its
 // header record goes to global scratch and its index to a deferred list, and
-//   K2 count   per-workgroup count of "first packet of a new key"
-//   K3 scan    exclusive scan of the counts (one workgroup) + NEXT_PORT
-//   K4 assign  ballot/popcount prefix -> ordinal -> port = base + ordinal
-//   K5 rewrite the deferred frames (the same quad rewrite, list-driven) + commit
-// finish them.  When no key is new (the steady state) K2..K5 see an empty
-// deferred list and return at once.  Kernel boundaries are the only
+//   K2 order   per 256-packet chunk: count the first packets of new keys,
+//              decoupled look-back scan of the counts, port = NEXT_PORT +
+//              ordinal (ballot/popcount rank within the chunk)
+//   K5 rewrite the deferred frames (the same quad rewrite, list-driven),
+//              commit the keys, advance NEXT_PORT
+// finish them.  When no key is new (the steady state) K2 and K5 see an
+// empty deferred list and return at once.  Kernel boundaries are the only
 // cross-workgroup hand-offs besides device-scope atomics on the table.
 #include "capsule_gpu.h"
 #include "device_common.hpp"
@@ -756,89 +757,77 @@ __device__ __forceinline__ bool is_first_new(const Nat64Args &a, uint32_t i) {
   return a.pm.slots[ps & kSlotMask].w[7] == i;
 }
 
-// ---- K2: per-block count of first packets of new keys ----------------------
-__global__ __launch_bounds__(kBlock) void nat64_count(Nat64Args a) {
-  if (a.pm.state[4u + a.par] == 0u) return;  // nothing deferred: K3 ignores block_sums
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  const bool f = i < a.n && is_first_new(a, i);
-  const int c = __syncthreads_count(f);
-  if (threadIdx.x == 0) a.block_sums[blockIdx.x] = (uint32_t)c;
-}
+// ---- K2: count, scan and assign in one pass (decoupled look-back) ---------
+// Chunk b (256 packets) counts its "first packet of a new key", publishes
+// the count, and looks back over the earlier chunks' published counts until
+// it meets an inclusive prefix; its first packets then get port = NEXT_PORT +
+// ordinal (ordinal = prefix + rank in the chunk).  Chunks are numbered by an
+// atomic ticket taken when the workgroup starts, so every chunk a workgroup
+// waits for belongs to a workgroup that is already running: no deadlock.
+// Look-back words: epoch << 34 | status << 32 | count (status 1 aggregate,
+// 2 inclusive; a word from an earlier call has another epoch = not yet).
+// NEXT_PORT itself is advanced by K5, after every assignment has read it.
+constexpr uint64_t kLbAgg = 1ull << 32, kLbIncl = 2ull << 32;
 
-// ---- K3: exclusive scan of block counts + NEXT_PORT update (1 workgroup) ---
-constexpr uint32_t kScanBlock = 1024;
-__global__ __launch_bounds__(kScanBlock) void nat64_scan(Nat64Args a, uint32_t nb) {
-  __shared__ uint32_t wsum[kScanBlock / 64];
-  __shared__ uint32_t carry;
-  if (a.pm.state[4u + a.par] == 0u) {  // no new key in this batch
-    if (threadIdx.x == 0) {
-      a.pm.state[2] = a.pm.state[0];
-      a.pm.state[3] = 0u;
-    }
-    return;
-  }
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  for (uint32_t base = 0; base < nb; base += kScanBlock) {
-    const uint32_t idx = base + threadIdx.x;
-    const uint32_t v = idx < nb ? a.block_sums[idx] : 0u;
-    uint32_t x = v;  // inclusive wave scan
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(x, d, 64);
-      if (lane >= (uint32_t)d) x += y;
-    }
-    if (lane == 63u) wsum[wave] = x;
-    __syncthreads();
-    uint32_t wpre = 0;
-    for (uint32_t w = 0; w < wave; ++w) wpre += wsum[w];
-    const uint32_t c0 = carry;
-    if (idx < nb) a.block_sums[idx] = c0 + wpre + x - v;
-    __syncthreads();
-    if (threadIdx.x == kScanBlock - 1) carry = c0 + wpre + x;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const uint32_t total = carry;
-    const uint32_t base_port = a.pm.state[0];
-    a.pm.state[2] = base_port;
-    a.pm.state[3] = total;
-    a.pm.state[0] = (base_port + total) & 0xffffu;  // AtomicU16 wrap
-    a.pm.state[1] += total;
-  }
-}
-
-// ---- K4: ordinal -> port for the first packet of each new key --------------
-__global__ __launch_bounds__(kBlock) void nat64_assign(Nat64Args a) {
+__global__ __launch_bounds__(kBlock) void nat64_order(Nat64Args a, uint32_t nb) {
+  __shared__ uint32_t s_chunk, s_prefix;
   __shared__ uint32_t wcount[kBlock / 64];
-  if (a.pm.state[4u + a.par] == 0u) return;
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (a.pm.state[4u + a.par] == 0u) return;  // nothing deferred: no new key
+  if (threadIdx.x == 0) s_chunk = atomicAdd(&a.pm.state[6u + a.par], 1u);
+  __syncthreads();
+  const uint32_t b = s_chunk;
+  const uint32_t i = b * kBlock + threadIdx.x;
   const bool f = i < a.n && is_first_new(a, i);
   const uint64_t mask = __ballot(f);
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t below = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
   if (lane == 0) wcount[wave] = (uint32_t)__popcll(mask);
+  const uint32_t c = (uint32_t)__syncthreads_count(f);
+  if (threadIdx.x == 0) {
+    const uint64_t ep = (uint64_t)(a.epoch & 0x3fffffffu) << 34;
+    uint32_t prefix = 0;
+    if (b == 0) {
+      __hip_atomic_store(&a.lookback[0], ep | kLbIncl | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(&a.lookback[b], ep | kLbAgg | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t j = b - 1;; --j) {
+        uint64_t v;
+        do {
+          v = __hip_atomic_load(&a.lookback[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } while ((v & ~0x3ffffffffull) != ep || (v & (3ull << 32)) == 0ull);
+        prefix += (uint32_t)v;
+        if (v & kLbIncl) break;
+      }
+      __hip_atomic_store(&a.lookback[b], ep | kLbIncl | (prefix + c), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_prefix = prefix;
+    if (b == nb - 1u) a.pm.state[8] = prefix + c;  // the batch's new keys, for K5
+  }
   __syncthreads();
-  uint32_t pre = a.block_sums[blockIdx.x];
+  uint32_t pre = s_prefix;
   for (uint32_t w = 0; w < wave; ++w) pre += wcount[w];
   if (f) {
     const uint32_t ps = a.pkt_slot[i], slot = ps & kSlotMask;
     const uint32_t ordinal = pre + below;
-    const uint32_t port = (a.pm.state[2] + ordinal) & 0xffffu;
+    const uint32_t port = (a.pm.state[0] + ordinal) & 0xffffu;  // NEXT_PORT.fetch_add order
     a.pm.slots[slot].w[6] = port;
     a.pkt_slot[i] = ps | kFirstBit;
     // ADDR_MAP.insert_new(port, key) (main.rs:50): the first mapping of a
     // port wins, also after NEXT_PORT wraps; ordinals are global
-    const uint64_t tag = ((uint64_t)(a.pm.state[1] - a.pm.state[3] + ordinal) << 32) | slot;
+    const uint64_t tag = ((uint64_t)(a.pm.state[1] + ordinal) << 32) | slot;
     atomicMin((unsigned long long *)&a.pm.rev[port], (unsigned long long)tag);
   }
 }
 
-
 // ---- K5: the deferred frames (phase 2's rewrite, list-driven) + commit -------
 __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_deferred(Nat64Args a) {
   const uint32_t cnt = a.pm.state[4u + a.par];
+  if (cnt != 0u && blockIdx.x == 0 && threadIdx.x == 0) {  // advance NEXT_PORT (AtomicU16 wrap)
+    const uint32_t total = a.pm.state[8];
+    a.pm.state[0] = (a.pm.state[0] + total) & 0xffffu;
+    a.pm.state[1] += total;
+  }
   const uint32_t g = threadIdx.x % kFG;
   const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
   const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
@@ -867,7 +856,10 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_deferred(Nat64Arg
     }
   }
   // the other parity's list counter is the next call's: clear it for that call
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.pm.state[4u + (a.par ^ 1u)] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.pm.state[4u + (a.par ^ 1u)] = 0u;  // deferred-list counter
+    a.pm.state[6u + (a.par ^ 1u)] = 0u;  // chunk ticket
+  }
 }
 
 // ============================ 4to6 direction =================================
@@ -999,6 +991,9 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
     pm.state[3] = 0u;
     pm.state[4] = 0u;  // deferred-list counters, by call parity
     pm.state[5] = 0u;
+    pm.state[6] = 0u;  // look-back chunk tickets, by call parity
+    pm.state[7] = 0u;
+    pm.state[8] = 0u;  // new keys of the last batch
   }
 }
 
@@ -1017,9 +1012,7 @@ hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s) {
   const uint32_t nb = nat64_num_blocks(a.n);
   const uint32_t nbq = (a.n + kBlock / kFG - 1) / (kBlock / kFG);  // one quad per frame
   hipLaunchKernelGGL(nat64_6to4_fused, dim3(nbq), dim3(kBlock), 0, s, a);
-  hipLaunchKernelGGL(nat64_count, dim3(nb), dim3(kBlock), 0, s, a);
-  hipLaunchKernelGGL(nat64_scan, dim3(1), dim3(kScanBlock), 0, s, a, nb);
-  hipLaunchKernelGGL(nat64_assign, dim3(nb), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(nat64_order, dim3(nb), dim3(kBlock), 0, s, a, nb);
   hipLaunchKernelGGL(nat64_6to4_deferred, dim3(nbq < 2048u ? nbq : 2048u), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
