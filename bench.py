@@ -384,14 +384,15 @@ def e2e_mbufs(args):
     ingress = {"stage": N.INGRESS_STAGE, "zero_copy": N.INGRESS_ZERO_COPY}[args.ingress]
     B = min(args.burst, n)
     bursts = [mbufs[s:s + B] for s in range(0, n - B + 1, B)]
-    outs = [(np.zeros(B, np.uint32), np.zeros(B, np.uint64)) for _ in range(2)]
+    outs = [(np.zeros(B, np.uint32), np.zeros(B, np.uint32), np.zeros(B, np.uint64))
+            for _ in range(2)]
     L = N.lib()
 
-    def call(k):
+    def call(k):  # the device-resident config's work: parse + checksums + hash
         mb = bursts[k % len(bursts)]
-        meta, fh = outs[k & 1]
+        meta, cs, fh = outs[k & 1]
         N.check(L.cgpu_parse_mbufs(ctx.handle, mb.ctypes.data, B, w["flags"], ingress,
-                                   meta.ctypes.data, None, fh.ctypes.data, None),
+                                   meta.ctypes.data, cs.ctypes.data, fh.ctypes.data, None),
                 "cgpu_parse_mbufs")
 
     for k in range(3):

@@ -9,7 +9,7 @@
 // buf_addr + data_off .. + data_len, first segment only, as Mbuf::data_len /
 // data_address / read_data (core/src/dpdk/mbuf.rs:196-205, 313-327).
 //
-// One lane per mbuf reads its header (one PCIe round trip), the wave
+// Quads of lanes read the mbuf headers (one 64-B request per mbuf), the wave
 // allocates its slots with one atomic, and then 16-lane groups copy four
 // frames at a time, 16 B per lane, all of a wave's first-256-B loads in
 // flight before any store.  Every host address is translated through the
@@ -54,19 +54,45 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   const bool valid = i < g.n;
-  // --- the mbuf header: buf_addr, data_off, data_len --------------------------
+  // --- the mbuf header: buf_addr @0, data_off @16, data_len @40 --------------
+  // Read cooperatively: in round r the quad of lanes 4m..4m+3 loads bytes
+  // 0..47 of mbuf 16r + m as three 16-B pieces of one 64-B segment (one PCIe
+  // read request instead of three small ones per mbuf); the owner lane then
+  // picks its fields up with ds_bpermute.
+  uint64_t dm = 0;
+  const bool mok = valid && translate(g, g.mbufs[i], CGPU_MBUF_SIZE, dm);
+  if (valid && !mok) atomicAdd(g.bad, 1u);
+  const uint32_t q = lane & 3u;
+  u32x4 H[4];
+#pragma unroll
+  for (uint32_t r = 0; r < 4u; ++r) {
+    const uint32_t m = 16u * r + (lane >> 2);
+    const uint64_t dmm = __shfl(dm, (int)m);
+    const bool okm = __shfl((int)mok, (int)m) != 0;
+    H[r] = u32x4{0u, 0u, 0u, 0u};
+    if (okm && q < 3u) H[r] = *reinterpret_cast<const u32x4 *>(dmm + 16u * q);
+  }
+  const uint32_t r_own = lane >> 4, src_lane = 4u * (lane & 15u);
+  uint32_t ba_lo = 0, ba_hi = 0, doff = 0, dlen = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < 4u; ++r) {
+    const uint32_t lo = __shfl(H[r][0], (int)src_lane), hi = __shfl(H[r][1], (int)src_lane);
+    const uint32_t d16 = __shfl(H[r][0], (int)(src_lane + 1u));  // bytes 16..19
+    const uint32_t d40 = __shfl(H[r][2], (int)(src_lane + 2u));  // bytes 40..43
+    if (r == r_own) {
+      ba_lo = lo;
+      ba_hi = hi;
+      doff = d16 & 0xffffu;
+      dlen = d40 & 0xffffu;
+    }
+  }
   uint64_t src = 0;
   uint32_t L = 0;
   bool ok = false;
-  if (valid) {
-    uint64_t dm;
-    if (translate(g, g.mbufs[i], CGPU_MBUF_SIZE, dm)) {
-      const uint64_t buf_addr = *reinterpret_cast<const uint64_t *>(dm + CGPU_MBUF_BUF_ADDR_OFF);
-      const uint32_t data_off = *reinterpret_cast<const uint16_t *>(dm + CGPU_MBUF_DATA_OFF_OFF);
-      const uint32_t data_len = *reinterpret_cast<const uint16_t *>(dm + CGPU_MBUF_DATA_LEN_OFF);
-      ok = data_len == 0u || translate(g, buf_addr + data_off, data_len, src);
-      L = ok ? data_len : 0u;
-    }
+  if (mok) {
+    const uint64_t buf_addr = ((uint64_t)ba_hi << 32) | ba_lo;
+    ok = dlen == 0u || translate(g, buf_addr + doff, dlen, src);
+    L = ok ? dlen : 0u;
     if (!ok) atomicAdd(g.bad, 1u);
   }
   // --- slots: one atomic per wave, prefix within the wave ---------------------
