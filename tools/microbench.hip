@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <vector>
 
 #include "capsule_gpu.h"
@@ -310,9 +311,43 @@ int main(int argc, char **argv) {
   for (auto &c : cases) {
     time_it(c.name, algo, [&](int r) {
       cgpu_batch b = {arena[r], bytes, off[r], len[r], n};
-      cgpu_parse_out o = {meta, c.csum_out ? csum : nullptr, hash, nullptr};
+      cgpu_parse_out o = {meta, c.csum_out ? csum : nullptr, hash, nullptr, nullptr};
       if (cgpu_parse_batch(ctx, &b, c.flags, &o, st)) { fprintf(stderr, "parse\n"); exit(2); }
     });
+  }
+  {  // the bench config with consecutive launches alternating between 2 / 4
+     // streams (independent bursts, as separate RX queues would submit them):
+     // wall time per launch over the timed run
+    const uint32_t fl = CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_UDP | CGPU_F_CSUM_IP | CGPU_F_CSUM_L4 | CGPU_F_FLOW_HASH;
+    for (int ns : {1, 2, 4}) {
+      hipStream_t ss[4];
+      uint32_t *m2[4];
+      uint64_t *h2[4];
+      for (int q = 0; q < ns; ++q) {
+        CK(hipStreamCreateWithFlags(&ss[q], hipStreamNonBlocking));
+        CK(hipMalloc(&m2[q], 4ull * n));
+        CK(hipMalloc(&h2[q], 8ull * n));
+      }
+      auto go = [&](int k) {
+        cgpu_batch b = {arena[k % R], bytes, off[k % R], len[k % R], n};
+        cgpu_parse_out o = {m2[k % ns], nullptr, h2[k % ns], nullptr, nullptr};
+        if (cgpu_parse_batch(ctx, &b, fl, &o, ss[k % ns])) { fprintf(stderr, "parse\n"); exit(2); }
+      };
+      for (int k = 0; k < 20; ++k) go(k);
+      CK(hipDeviceSynchronize());
+      auto t0 = std::chrono::steady_clock::now();
+      for (int k = 0; k < iters; ++k) go(k);
+      CK(hipDeviceSynchronize());
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / iters;
+      printf("{\"case\": \"parse_verify_hash_streams%d_wall\", \"us\": %.3f, \"GBps\": %.1f, \"Mpps\": %.1f}\n", ns, us,
+             algo / (us * 1e-6) / 1e9, n / us);
+      fflush(stdout);
+      for (int q = 0; q < ns; ++q) {
+        CK(hipStreamDestroy(ss[q]));
+        CK(hipFree(m2[q]));
+        CK(hipFree(h2[q]));
+      }
+    }
   }
   {  // nat64-shaped copies over 1M x 256-B frames (separate, larger arena)
     const uint32_t nf = n;
