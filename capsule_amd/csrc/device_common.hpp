@@ -216,34 +216,80 @@ __device__ __forceinline__ uint64_t sip_finish(Sip &s, W64 b) {
   return (uint64_t)r.lo | ((uint64_t)r.hi << 32);
 }
 
+// The first compressions of both families absorb constant words (the IpAddr
+// discriminant, and for v6 the slice length 16), so the state after them is a
+// compile-time constant: sip_const evaluates SipHash on the host compiler.
+struct SipC {
+  uint64_t v0, v1, v2, v3;
+};
+
+constexpr uint64_t rotl_c(uint64_t x, int b) { return (x << b) | (x >> (64 - b)); }
+
+constexpr SipC sip_round_c(SipC s) {
+  s.v0 += s.v1;
+  s.v1 = rotl_c(s.v1, 13) ^ s.v0;
+  s.v0 = rotl_c(s.v0, 32);
+  s.v2 += s.v3;
+  s.v3 = rotl_c(s.v3, 16) ^ s.v2;
+  s.v0 += s.v3;
+  s.v3 = rotl_c(s.v3, 21) ^ s.v0;
+  s.v2 += s.v1;
+  s.v1 = rotl_c(s.v1, 17) ^ s.v2;
+  s.v2 = rotl_c(s.v2, 32);
+  return s;
+}
+
+constexpr SipC sip_block_c(SipC s, uint64_t m) {
+  s.v3 ^= m;
+  s = sip_round_c(s);
+  s.v0 ^= m;
+  return s;
+}
+
+constexpr SipC kSipInit{0x736f6d6570736575ull, 0x646f72616e646f6dull, 0x6c7967656e657261ull,
+                        0x7465646279746573ull};
+constexpr SipC kSip4 = sip_block_c(kSipInit, 0);                   // v4: [disc 0]
+constexpr SipC kSip6 = sip_block_c(sip_block_c(kSipInit, 1), 16);  // v6: [disc 1][16u64]
+
+__device__ __forceinline__ Sip sip_from(const SipC &c) {
+  return Sip{w64(c.v0), w64(c.v1), w64(c.v2), w64(c.v3)};
+}
+
 // Hash of Flow{src_ip, dst_ip, src_port, dst_port, protocol} as Rust 1.50
 // `#[derive(Hash)]` feeds it to DefaultHasher:
 //   v4: [0u64][src 4B][0u64][dst 4B][sport le16][dport le16][proto]  = 29 B
 //   v6: [1u64][16u64][src 16B][1u64][16u64][dst 16B][ports][proto]   = 69 B
 // Addresses are the little-endian dwords of their wire bytes; sport/dport
-// are host-order values.  v4 and v6 share the first three compressions'
-// code (blocks 0,1,2 differ only in their words), so a wave that mixes the
-// families pays 5 extra compressions for its v6 lanes instead of a second
-// full hash.
+// are host-order values.  The constant leading blocks start from kSip4 /
+// kSip6.  An all-IPv4 wave (uniform branch) runs 2 compressions + finish on
+// constants the compiler folds further (the first block's v0/v1/v2 are
+// constant); a mixed wave shares the next two compressions' code and pays 4
+// extra ones for its v6 lanes.
 __device__ __forceinline__ uint64_t flow_hash(bool v6, const uint32_t (&src)[4],
                                               const uint32_t (&dst)[4], uint32_t sport,
                                               uint32_t dport, uint32_t proto) {
-  Sip s = sip_init();
-  // block 0: v4 [disc 0] ; v6 [disc 1]
-  sip_block(s, W64{v6 ? 1u : 0u, 0u});
-  // block 1: v4 [src][disc lo 0] ; v6 [16u64]
-  sip_block(s, W64{v6 ? 16u : src[0], 0u});
-  // block 2: v4 [disc hi 0][dst] ; v6 [src 0..7]
-  sip_block(s, v6 ? W64{src[0], src[1]} : W64{0u, dst[0]});
+  Sip s;
+  if (!__ballot(v6)) {
+    s = sip_from(kSip4);
+    sip_block(s, W64{src[0], 0u});  // [src][disc lo 0]
+    sip_block(s, W64{0u, dst[0]});  // [disc hi 0][dst]
+    return sip_finish(s, W64{sport | (dport << 16), proto | (29u << 24)});
+  }
+  const Sip s4 = sip_from(kSip4), s6 = sip_from(kSip6);
+  s.v0 = v6 ? s6.v0 : s4.v0;
+  s.v1 = v6 ? s6.v1 : s4.v1;
+  s.v2 = v6 ? s6.v2 : s4.v2;
+  s.v3 = v6 ? s6.v3 : s4.v3;
+  // v4 [src][disc lo 0] [disc hi 0][dst] ; v6 [src 0..7] [src 8..15]
+  sip_block(s, W64{src[0], v6 ? src[1] : 0u});
+  sip_block(s, v6 ? W64{src[2], src[3]} : W64{0u, dst[0]});
   if (v6) {
-    sip_block(s, W64{src[2], src[3]});
     sip_block(s, W64{1u, 0u});
     sip_block(s, W64{16u, 0u});
     sip_block(s, W64{dst[0], dst[1]});
     sip_block(s, W64{dst[2], dst[3]});
   }
-  const W64 b{sport | (dport << 16), proto | ((v6 ? 69u : 29u) << 24)};
-  return sip_finish(s, b);
+  return sip_finish(s, W64{sport | (dport << 16), proto | ((v6 ? 69u : 29u) << 24)});
 }
 
 }  // namespace cgpu
