@@ -48,6 +48,13 @@ def make_workload(cfg, seed):
         desc = "1M x 64B Eth/IPv4/UDP: parse + IPv4/UDP checksum verify + 5-tuple hash"
         return dict(arena=arena, off=off, len=ln, flags=flags, kind="parse", desc=desc,
                     algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame="64B")
+    if cfg in ("parse256", "parse1500"):  # the metric's other frame sizes, same work as parse64
+        size = 256 if cfg == "parse256" else 1500
+        arena, off, ln = synth.uniform(n, frame_len=size, seed=seed, slot=(size + 63) // 64 * 64)
+        flags = N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP | N.F_CSUM_L4 | N.F_FLOW_HASH
+        desc = f"1M x {size}B Eth/IPv4/UDP: parse + IPv4/UDP checksum verify + 5-tuple hash"
+        return dict(arena=arena, off=off, len=ln, flags=flags, kind="parse", desc=desc,
+                    algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame=f"{size}B")
     if cfg == "imix":
         return imix_header_bytes_workload(seed)
     if cfg == "imix_csum":
@@ -206,7 +213,8 @@ def main():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="parse64",
-                    choices=["parse64", "imix", "imix_csum", "nat64", "nat64_4to6"])
+                    choices=["parse64", "parse256", "parse1500", "imix", "imix_csum", "nat64",
+                             "nat64_4to6"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--graph", action="store_true",
@@ -233,8 +241,8 @@ def main():
     g = ShardGroup()
     dev = torch.device("cuda", g.local_rank)
     torch.cuda.set_device(dev)
-    seed = g.shard_seed(0xC0FFEE + {"parse64": 2, "imix": 3, "imix_csum": 3, "nat64": 4,
-                                    "nat64_4to6": 4}[args.config])
+    seed = g.shard_seed(0xC0FFEE + {"parse64": 2, "parse256": 2, "parse1500": 2, "imix": 3,
+                                    "imix_csum": 3, "nat64": 4, "nat64_4to6": 4}[args.config])
     w = make_workload(args.config, seed)
     n = len(w["off"])
     ctx = packets.Context(g.local_rank)

@@ -45,6 +45,10 @@ constexpr uint32_t kBlock = CGPU_PARSE_BLOCK;
 constexpr int kWin = 24;        // packet-relative window dwords (96 B)
 constexpr uint32_t kQEnd = 88;  // normalized window bytes valid after a QinQ shift
 constexpr uint32_t kNoRead = 0xffffff00u;  // > any arena_len the ABI accepts
+#ifndef CGPU_SLOT_PIECES
+#define CGPU_SLOT_PIECES 2
+#endif
+constexpr uint32_t kSlotPieces = CGPU_SLOT_PIECES;  // longest tail (256-B pieces) summed in slots
 
 __device__ __forceinline__ uint32_t sel3(uint32_t k, uint32_t a, uint32_t b, uint32_t c) {
   return k == 0u ? a : (k == 1u ? b : c);
@@ -122,6 +126,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
 
   // --- the packet-relative window P ---------------------------------------
   uint32_t P[kWin];
+  uint32_t wlim = 96u;  // packet bytes the window holds
   const bool slow = (off & 3u) != 0u || (uint64_t)off + 96u > (uint64_t)a.arena_len;
   if (__ballot(slow)) {
     load_window_general(rs, a.arena_len, off, len, P);
@@ -134,31 +139,36 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       P[4 * c + 2] = v[2];
       P[4 * c + 3] = v[3];
     }
-    // Bytes 64..95, per lane: with an L4 checksum every frame that reaches a
-    // chunk needs it; without, only frames whose headers end past byte 64
-    // (IPv6/TCP, or IPv6 behind VLAN tags) -- decided from the first 64 B, so
-    // every other frame stays at one 64-B segment.  An instruction is skipped
-    // when no lane of the wave needs it.
-    uint32_t hdr_end = 96u;
-    if (!L4C) {
+    // Bytes 64..95, per lane, only where a frame's headers end past byte 64
+    // (IPv6/TCP, or IPv6 behind VLAN tags) -- decided from the first 64 B --
+    // or, with an L4 checksum, where the whole frame fits in 96 B.  A longer
+    // frame's checksum span continues at byte 64 in the coalesced tail loop,
+    // so it pays no strided loads past its first 64 B.  An instruction is
+    // skipped when no lane of the wave needs it.
+    wlim = 64u;
+    if (__ballot(len > 64u)) {
       const uint32_t mk = be16_lo(P[3]);
       const uint32_t kk = mk == 0x8100u ? 1u : (mk == 0x88a8u ? 2u : 0u);
       const uint32_t et = be16_lo(sel3(kk, P[3], P[4], P[5]));
       const uint32_t w5 = sel3(kk, P[5], P[6], P[7]);  // normalized bytes 20..23
       const bool is6 = et == 0x86ddu;
       const uint32_t pr = is6 ? (w5 & 0xffu) : (w5 >> 24);
-      hdr_end = (is6 ? 54u + 4u * kk : 0u) + (pr == 6u ? 20u : 8u);
-    }
+      const uint32_t hdr_end = (is6 ? 54u + 4u * kk : 0u) + (pr == 6u ? 20u : 8u);
 #pragma unroll
-    for (int c = 4; c < 6; ++c) {
-      const bool need = len > 16u * c && hdr_end > 16u * c;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (__ballot(need))
-        v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(need ? off + 16u * c : kNoRead), 0, 0);
-      P[4 * c] = v[0];
-      P[4 * c + 1] = v[1];
-      P[4 * c + 2] = v[2];
-      P[4 * c + 3] = v[3];
+      for (int c = 4; c < 6; ++c) {
+        const bool need = len > 16u * c && (hdr_end > 16u * c || (L4C && len <= 96u));
+        if (need) wlim = 16u * c + 16u;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (__ballot(need))
+          v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(need ? off + 16u * c : kNoRead), 0, 0);
+        P[4 * c] = v[0];
+        P[4 * c + 1] = v[1];
+        P[4 * c + 2] = v[2];
+        P[4 * c + 3] = v[3];
+      }
+    } else {
+#pragma unroll
+      for (int j = 16; j < kWin; ++j) P[j] = 0u;
     }
   }
 
@@ -301,7 +311,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     ip_c = (~swap16(fold32(s))) & 0xffffu;
     if (ip_c == swap16(Q[6] & 0xffffu)) meta |= CGPU_META_IP_CSUM_OK;
   }
-  uint32_t s = 0, stored_le = 0;
+  uint32_t s = 0, stored_le = 0, t_b = 0;
   bool has_tail = false;
   if (L4C && l4_ok) {
     // pseudo-header addresses + span [l4, len) (udp.rs:204-219, tcp.rs:
@@ -310,7 +320,10 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     s = sad16(v6 ? (Q[5] & 0xffff0000u) : 0u, 0u);
     s = sad16(v6 ? Q[6] : (Q[6] & 0xffff0000u), s);
     const uint32_t endn = len - 4u * k;  // normalized end of frame
-    const uint32_t wend = endn < kQEnd ? endn : kQEnd;
+    // A span longer than the window is split at a 16-B aligned arena offset:
+    // the window sums up to it, the tail loop below sums whole chunks from it.
+    const uint32_t wq = wlim - 4u * k < kQEnd ? wlim - 4u * k : kQEnd;  // normalized window limit
+    const uint32_t wend = endn <= wq ? endn : wq - ((off + wq + 4u * k) & 15u);
     if (!__ballot(wend != __builtin_amdgcn_readfirstlane(wend))) {
       s = sum_to_end<7>(Q, __builtin_amdgcn_readfirstlane(wend), s);  // scalar masks
     } else {
@@ -323,7 +336,8 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     // ICMPv4 has no pseudo-header (icmp/v4/mod.rs:118-129): take the
     // addresses (bytes 26..33) back out of the exact sum
     if (icmp && !v6) s -= (Q[6] >> 16) + (Q[7] & 0xffffu) + (Q[7] >> 16) + (Q[8] & 0xffffu);
-    has_tail = endn > kQEnd;  // span continues past the window
+    has_tail = endn > wq;  // span continues past the window
+    t_b = off + 4u * k + wend;  // where it continues (16-B aligned)
     if (xok) {
       // Behind an extension header: src + (segments[0] behind a routing
       // header, else dst) + the span [l4_off, len) read from memory.  Sums mod
@@ -462,21 +476,89 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     out[2] = e2;
   }
   if (L4C && __ballot(has_tail)) {
-    // The tails of the wave's long frames (bytes past the register window) are
-    // summed by 16-lane groups, four frames at a time: in round r group j takes
-    // the (4r + j)-th long frame of the wave.  Its lanes load 16-B chunks
-    // 256 B apart, four per step in flight, sum them without masks, subtract
-    // the bytes of the first and last chunk that lie outside the tail, and the
-    // row reduces; the owner lane picks its sum up with a bpermute.
-    const uint32_t t_from = off + kQEnd + 4u * k, t_to = off + len;
+    // Tails: the span past the window, from the 16-B aligned offset t_b to
+    // the frame end, summed in 16-B chunks by 16-lane rows (a row reads 256
+    // contiguous bytes per load) and reduced per frame.
+    const uint32_t t_to = off + len;
     const uint32_t lane = threadIdx.x & 63u, grp = lane >> 4, l16 = lane & 15u;
-    const uint64_t mall = __ballot(has_tail);
-    const uint32_t my_rank =
-        __builtin_amdgcn_mbcnt_hi((uint32_t)(mall >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mall, 0u));
+    const uint32_t pieces = has_tail ? (t_to - t_b + 255u) >> 8 : 0u;  // 256-B pieces
+    const bool slot_tail = has_tail && pieces <= kSlotPieces;
     // every chunk any tail needs lies inside the arena: branch-free loads
     const bool fast = !__ballot(has_tail && (uint64_t)((t_to + 15u) & ~15u) > (uint64_t)a.arena_len);
     uint32_t tail = 0;
-    uint64_t m = mall;
+    // Short tails (at most kSlotPieces pieces): a round fills 16 slots, one
+    // piece each, in frame order from a wave-uniform cursor (SALU); row g
+    // takes slots g, 4 + g, 8 + g, 12 + g, so a lane has four loads in
+    // flight.  A piece's row sum is formed with DPP row shifts and added by
+    // its frame's lane; a frame's last chunk is masked at the frame end.
+    uint64_t m = __ballot(slot_tail);
+    if (m) {
+      uint32_t cur = (uint32_t)__builtin_ctzll(m), cur_piece = 0;
+      uint32_t cur_n = __builtin_amdgcn_readlane(pieces, cur);
+      while (cur < 64u) {
+        uint32_t sf[16], sp[16];  // slot -> (frame lane, piece), wave-uniform
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          sf[q] = cur;
+          sp[q] = cur_piece;
+          if (cur < 64u && ++cur_piece == cur_n) {
+            m &= m - 1u;
+            cur = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+            cur_piece = 0;
+            cur_n = cur < 64u ? __builtin_amdgcn_readlane(pieces, cur) : 0u;
+          }
+        }
+        uint32_t acc[4];
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const uint32_t f =
+              grp == 0u ? sf[4 * it] : (grp == 1u ? sf[4 * it + 1] : (grp == 2u ? sf[4 * it + 2] : sf[4 * it + 3]));
+          const uint32_t pc =
+              grp == 0u ? sp[4 * it] : (grp == 1u ? sp[4 * it + 1] : (grp == 2u ? sp[4 * it + 2] : sp[4 * it + 3]));
+          const bool live = f < 64u;
+          const uint32_t fb = __shfl(t_b, live ? f : 0u), ft = __shfl(t_to, live ? f : 0u);
+          const uint32_t o = fb + 256u * pc + 16u * l16;
+          const bool need = live && o < ft;
+          u32x4 v;
+          if (fast) {
+            v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(need ? o : kNoRead), 0, 0);
+          } else {
+            v = u32x4{0u, 0u, 0u, 0u};
+            if (need) v = load16(rs, o, a.arena_len);
+          }
+          const uint32_t rem = need ? ft - o : 16u;  // bytes of the chunk inside the frame
+          if (__ballot(rem < 16u)) {
+#pragma unroll
+            for (uint32_t t = 0; t < 4u; ++t) {
+              const uint32_t lo = 4u * t;
+              v[t] &= rem >= lo + 4u ? 0xffffffffu : (rem <= lo ? 0u : 0xffffffffu >> (8u * (lo + 4u - rem)));
+            }
+          }
+          uint32_t x = sum4(v, 0u);
+          x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+          x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+          x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+          x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+          acc[it] = x;  // lane 16 g + 15 holds slot 4 it + g's sum
+        }
+#pragma unroll
+        for (int it = 0; it < 4; ++it)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const uint32_t x = __builtin_amdgcn_readlane(acc[it], 16 * g + 15);
+            if (lane == sf[4 * it + g]) tail += x;
+          }
+      }
+    }
+    // Long tails: 16-lane group j takes the (4r + j)-th long frame of the
+    // wave in round r and walks it 1 KiB at a time, four loads 256 B apart in
+    // flight; the row reduces and the owner lane picks its sum up with a
+    // bpermute.
+    const bool long_tail = has_tail && !slot_tail;
+    const uint64_t mall = __ballot(long_tail);
+    const uint32_t my_rank =
+        __builtin_amdgcn_mbcnt_hi((uint32_t)(mall >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mall, 0u));
+    m = mall;
     for (uint32_t r = 0; m; ++r) {
       uint32_t own[4];
 #pragma unroll
@@ -490,11 +572,11 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       const uint32_t mine = grp == 0u ? own[0] : (grp == 1u ? own[1] : (grp == 2u ? own[2] : own[3]));
       const bool active = mine < 64u;
       const uint32_t src = active ? mine : 0u;
-      const uint32_t fr = __shfl(t_from, src), to = __shfl(t_to, src);
+      const uint32_t fr = __shfl(t_b, src), to = __shfl(t_to, src);
       uint32_t acc = 0;
       if (active) {
-        const uint32_t b = fr & ~15u, ct = (to - 1u) & ~15u;
-        for (uint32_t base = b; base < to; base += 1024u) {
+        const uint32_t ct = (to - 1u) & ~15u;
+        for (uint32_t base = fr; base < to; base += 1024u) {
           u32x4 v[4];
 #pragma unroll
           for (uint32_t it = 0; it < 4u; ++it) {
@@ -512,13 +594,13 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
 #pragma unroll
           for (uint32_t it = 0; it < 4u; ++it) {
             const uint32_t o = base + 256u * it + 16u * l16;
-            if (o == b || o == ct) acc -= chunk_excess(v[it], o, fr, to);
+            if (o == ct) acc -= chunk_excess(v[it], o, fr, to);  // fr is chunk-aligned
           }
         }
       }
 #pragma unroll
       for (uint32_t d = 8; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 16);
-      const bool mine_now = has_tail && my_rank >= 4u * r && my_rank < 4u * r + 4u;
+      const bool mine_now = long_tail && my_rank >= 4u * r && my_rank < 4u * r + 4u;
       const uint32_t got = __shfl(acc, mine_now ? (my_rank - 4u * r) * 16u : 0u);
       if (mine_now) tail = got;
     }

@@ -2,7 +2,7 @@
 # bench + rocprofv3 (stats, FETCH_SIZE, WRITE_SIZE) for every config.
 # usage: bash scripts/all_configs.sh <tag> [configs...]
 TAG=${1:-r03}; shift
-CONFIGS=${*:-parse64 imix imix_csum nat64 nat64_4to6}
+CONFIGS=${*:-parse64 parse256 parse1500 imix imix_csum nat64 nat64_4to6}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for c in $CONFIGS; do

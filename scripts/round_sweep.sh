@@ -3,7 +3,7 @@
 # config, then the end-to-end (host-resident, PCIe-inclusive) rates.
 # usage: bash scripts/round_sweep.sh <tag> [configs...]
 TAG=${1:-round1}; shift
-CONFIGS=${*:-parse64 imix imix_csum nat64 nat64_4to6}
+CONFIGS=${*:-parse64 parse256 parse1500 imix imix_csum nat64 nat64_4to6}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 bash scripts/all_configs.sh "$TAG" $CONFIGS || exit $?
