@@ -45,10 +45,11 @@ constexpr uint32_t kBlock = CGPU_PARSE_BLOCK;
 constexpr int kWin = 24;        // packet-relative window dwords (96 B)
 constexpr uint32_t kQEnd = 88;  // normalized window bytes valid after a QinQ shift
 constexpr uint32_t kNoRead = 0xffffff00u;  // > any arena_len the ABI accepts
-#ifndef CGPU_SLOT_PIECES
-#define CGPU_SLOT_PIECES 2
+constexpr uint32_t kSlotPieces = 2;  // longest tail (256-B pieces) summed in slots
+#ifndef CGPU_SLOT_IT
+#define CGPU_SLOT_IT 4
 #endif
-constexpr uint32_t kSlotPieces = CGPU_SLOT_PIECES;  // longest tail (256-B pieces) summed in slots
+constexpr uint32_t kSlotIt = CGPU_SLOT_IT;  // slots per 16-lane row and round (loads in flight)
 
 __device__ __forceinline__ uint32_t sel3(uint32_t k, uint32_t a, uint32_t b, uint32_t c) {
   return k == 0u ? a : (k == 1u ? b : c);
@@ -486,38 +487,33 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     // every chunk any tail needs lies inside the arena: branch-free loads
     const bool fast = !__ballot(has_tail && (uint64_t)((t_to + 15u) & ~15u) > (uint64_t)a.arena_len);
     uint32_t tail = 0;
-    // Short tails (at most kSlotPieces pieces): a round fills 16 slots, one
-    // piece each, in frame order from a wave-uniform cursor (SALU); row g
-    // takes slots g, 4 + g, 8 + g, 12 + g, so a lane has four loads in
-    // flight.  A piece's row sum is formed with DPP row shifts and added by
-    // its frame's lane; a frame's last chunk is masked at the frame end.
-    uint64_t m = __ballot(slot_tail);
-    if (m) {
-      uint32_t cur = (uint32_t)__builtin_ctzll(m), cur_piece = 0;
-      uint32_t cur_n = __builtin_amdgcn_readlane(pieces, cur);
-      while (cur < 64u) {
-        uint32_t sf[16], sp[16];  // slot -> (frame lane, piece), wave-uniform
+    // Short tails (one or two 256-B pieces): pass p sums piece p of every
+    // frame that has one.  The frames of a pass are compacted (ds_permute of
+    // their piece offset and end to lane rank), and a round takes 16 of
+    // them: row g sums slots g, 4 + g, 8 + g, 12 + g, one 16-B chunk per lane
+    // and slot, so a lane has four loads in flight and a row reads 256
+    // contiguous bytes.  A slot's row sum is formed with DPP row shifts and
+    // added by its frame's lane; a frame's last chunk is masked at its end.
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          sf[q] = cur;
-          sp[q] = cur_piece;
-          if (cur < 64u && ++cur_piece == cur_n) {
-            m &= m - 1u;
-            cur = m ? (uint32_t)__builtin_ctzll(m) : 64u;
-            cur_piece = 0;
-            cur_n = cur < 64u ? __builtin_amdgcn_readlane(pieces, cur) : 0u;
-          }
-        }
-        uint32_t acc[4];
+    for (uint32_t pass = 0; pass < kSlotPieces; ++pass) {
+      const bool in = slot_tail && pieces > pass;
+      const uint64_t mp = __ballot(in);
+      if (!mp) break;
+      const uint32_t n_f = (uint32_t)__builtin_popcountll(mp);
+      const uint32_t rank =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(mp >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mp, 0u));
+      const int to_addr = (int)(4u * (in ? rank : 63u));  // frames to their rank; others to lane 63
+      const uint32_t c_own = (uint32_t)__builtin_amdgcn_ds_permute(to_addr, (int)lane);
+      const uint32_t c_b = (uint32_t)__builtin_amdgcn_ds_permute(to_addr, (int)(t_b + 256u * pass));
+      const uint32_t c_e = (uint32_t)__builtin_amdgcn_ds_permute(to_addr, (int)t_to);
+      for (uint32_t base = 0; base < n_f; base += 4u * kSlotIt) {
+        uint32_t acc[kSlotIt];
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
-          const uint32_t f =
-              grp == 0u ? sf[4 * it] : (grp == 1u ? sf[4 * it + 1] : (grp == 2u ? sf[4 * it + 2] : sf[4 * it + 3]));
-          const uint32_t pc =
-              grp == 0u ? sp[4 * it] : (grp == 1u ? sp[4 * it + 1] : (grp == 2u ? sp[4 * it + 2] : sp[4 * it + 3]));
-          const bool live = f < 64u;
-          const uint32_t fb = __shfl(t_b, live ? f : 0u), ft = __shfl(t_to, live ? f : 0u);
-          const uint32_t o = fb + 256u * pc + 16u * l16;
+        for (uint32_t it = 0; it < kSlotIt; ++it) {
+          const uint32_t q = base + 4u * it + grp;
+          const bool live = q < n_f;
+          const uint32_t fb = __shfl(c_b, live ? q : 0u), ft = __shfl(c_e, live ? q : 0u);
+          const uint32_t o = fb + 16u * l16;
           const bool need = live && o < ft;
           u32x4 v;
           if (fast) {
@@ -539,14 +535,17 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
           x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, true);  // row_shr:2
           x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, true);  // row_shr:4
           x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, true);  // row_shr:8
-          acc[it] = x;  // lane 16 g + 15 holds slot 4 it + g's sum
+          acc[it] = x;  // lane 16 g + 15 holds slot base + 4 it + g
         }
 #pragma unroll
-        for (int it = 0; it < 4; ++it)
+        for (uint32_t it = 0; it < kSlotIt; ++it)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const uint32_t x = __builtin_amdgcn_readlane(acc[it], 16 * g + 15);
-            if (lane == sf[4 * it + g]) tail += x;
+          for (uint32_t g = 0; g < 4u; ++g) {
+            const uint32_t q = base + 4u * it + g;
+            if (q < n_f) {
+              const uint32_t x = __builtin_amdgcn_readlane(acc[it], 16 * g + 15);
+              if (lane == __builtin_amdgcn_readlane(c_own, q)) tail += x;
+            }
           }
       }
     }
@@ -558,7 +557,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     const uint64_t mall = __ballot(long_tail);
     const uint32_t my_rank =
         __builtin_amdgcn_mbcnt_hi((uint32_t)(mall >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mall, 0u));
-    m = mall;
+    uint64_t m = mall;
     for (uint32_t r = 0; m; ++r) {
       uint32_t own[4];
 #pragma unroll
