@@ -117,6 +117,27 @@ def test_every_length_boundary(ctx):
         assert_parity(ctx, arena, off + shift, ln, ALL | N.F_ACCEPT_ICMP)
 
 
+@pytest.mark.parametrize("slot,shift", [(16, 0), (64, 4), (256, 0), (64, 2)])
+def test_checksum_tail_lengths(ctx, slot, shift):
+    """Every frame length from 60 to 1300 B (and the 2048-B data room), v4/UDP
+    and v6/TCP, untagged and QinQ: the window / tail split at byte 64 or 96,
+    one- and two-piece slot tails (pieces of 256 B), the long-tail loop past
+    two pieces, and a last chunk that ends anywhere in its 16 B, at several
+    arena alignments of the frames."""
+    rng = np.random.default_rng(slot + shift)
+    frames = []
+    for kind, vlan in ((synth.V4_UDP, 0), (synth.V6_TCP, 0), (synth.V4_TCP, 2), (synth.V6_UDP, 1)):
+        hdr = 14 + 4 * vlan + (40 if kind[0] == 6 else 20) + (20 if kind[1] == 6 else 8)
+        lens = list(range(max(60, hdr), 1301)) + [2047, 2048]
+        for L in lens:
+            frames.append(bytes(synth.build_frames(rng, 1, kind, L, vlan)[0]))
+    order = rng.permutation(len(frames))  # mixed lengths within every wave
+    arena, off, ln = synth.pack_frames([frames[i] for i in order], slot)
+    arena = np.concatenate([np.zeros(shift, np.uint8), arena])
+    om = assert_parity(ctx, arena, off + shift, ln, ALL, fields=False)
+    assert ((om & 0xFF) == 0).all() and (om & N.META_L4_CSUM_OK).all()
+
+
 def test_packet_flush_with_arena_end(ctx):
     """Packets that end exactly at the end of the arena, at every alignment
     (the buffer-resource range check must return zeros, not fault)."""
