@@ -210,8 +210,10 @@ def cpu_baseline(w, seconds):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=50)
+    # ~40 ms of warmup brings the GPU to its steady clocks: with 50 warmup
+    # steps the 64-B config measured 18.5 us per launch, with 2000 17.2 us.
+    ap.add_argument("--steps", type=int, default=5000)
+    ap.add_argument("--warmup", type=int, default=2000)
     ap.add_argument("--config", default="parse64",
                     choices=["parse64", "parse256", "parse1500", "imix", "imix_csum", "nat64",
                              "nat64_4to6"])

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 mkdir -p $REPO/gpurun_out
 for v in "$@"; do
   for c in $CFGS; do
-    CAPSULE_GPU_LIB=$REPO/capsule_amd/var/$v.so timeout -k 10 200 python3 $REPO/bench.py --config $c --steps 200 --warmup 20 --no-cpu > $REPO/gpurun_out/ab_${v}_$c.log 2>&1 || { echo "$v $c failed"; tail -5 $REPO/gpurun_out/ab_${v}_$c.log; exit 1; }
+    CAPSULE_GPU_LIB=$REPO/capsule_amd/var/$v.so timeout -k 10 200 python3 $REPO/bench.py --config $c --steps ${AB_STEPS:-2000} --warmup 1000 --no-cpu > $REPO/gpurun_out/ab_${v}_$c.log 2>&1 || { echo "$v $c failed"; tail -5 $REPO/gpurun_out/ab_${v}_$c.log; exit 1; }
     python3 - $REPO/gpurun_out/ab_${v}_$c.log $v $c <<'PY'
 import json, sys
 r = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][0]
