@@ -147,6 +147,7 @@ static int check_batch(const cgpu_batch *b) {
   if (b->n == 0) return 0;
   if (!b->arena || !b->off || !b->len) return CGPU_EINVAL;
   if (b->arena_len > 0xffff0000ull) return CGPU_EINVAL;  // offsets above are "no read"
+  if (b->n > CGPU_MAX_BATCH) return CGPU_EINVAL;          // 32-bit descriptor byte offsets
   return 0;
 }
 

@@ -122,8 +122,12 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   // nothing, so the wave stays whole for the cooperative tail sum below.
   const bool valid = i < a.n;
   const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
-  const uint32_t off = valid ? a.off[i] : 0u;
-  const uint32_t len = valid ? (uint32_t)a.len[i] : 0u;
+  // descriptors through buffer resources: lanes past n read 0 (no branch)
+  const uint64_t nb = (uint64_t)a.n;
+  const rsrc_t r_off = make_rsrc(a.off, (uint32_t)(4u * nb < 0xffffffffull ? 4u * nb : 0xffffffffull));
+  const rsrc_t r_len = make_rsrc(a.len, (uint32_t)(2u * nb < 0xffffffffull ? 2u * nb : 0xffffffffull));
+  const uint32_t off = __builtin_amdgcn_raw_buffer_load_b32(r_off, (int)(4u * i), 0, 0);
+  const uint32_t len = __builtin_amdgcn_raw_buffer_load_b16(r_len, (int)(2u * i), 0, 0);
 
   // --- the packet-relative window P ---------------------------------------
   uint32_t P[kWin];

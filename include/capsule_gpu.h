@@ -131,7 +131,9 @@ enum cgpu_pkt_status {
  * A batch is an arena of packet bytes plus one (offset, data_len) pair per
  * packet: the device image of a burst of single-segment mbufs
  * (buf_addr + data_off, data_len; mbuf.rs:196-205).  All pointers are
- * device pointers for the *_batch entry points.  arena_len must be <= 0xFFFF0000.    */
+ * device pointers for the *_batch entry points.  arena_len must be <= 0xFFFF0000
+ * and n <= CGPU_MAX_BATCH.                                                   */
+#define CGPU_MAX_BATCH (1u << 30)
 typedef struct cgpu_batch {
   const uint8_t *arena;
   uint64_t arena_len;
