@@ -53,6 +53,11 @@ INGRESS_STAGE, INGRESS_ZERO_COPY = 0, 1
 
 KEY_U8, KEY_META_CLASS = 0, 1
 
+# cgpu_set_ip (Udp/Tcp::set_src_ip / set_dst_ip)
+SETIP_OK, SETIP_SKIPPED, SETIP_SRC_MISMATCH, SETIP_DST_MISMATCH = 0, 1, 2, 3
+IP_ADDR_FIELDS = [("octets", "u1", (16,)), ("family", "<u4")]  # cgpu_ip_addr
+IP_ADDR_SIZE = 20
+
 
 def meta_status(m):
     return m & 0xFF
@@ -119,7 +124,7 @@ EXPORTS = [
     "cgpu_portmap_create", "cgpu_portmap_destroy", "cgpu_portmap_next_port",
     "cgpu_portmap_size", "cgpu_nat64_6to4", "cgpu_nat64_4to6", "cgpu_group_by", "cgpu_last_error", "cgpu_strerror",
     "cgpu_pkt_status_str", "cgpu_abi_version", "cgpu_host_register", "cgpu_host_unregister",
-    "cgpu_parse_mbufs",
+    "cgpu_parse_mbufs", "cgpu_set_ip",
 ]
 
 _lib = None
@@ -171,6 +176,8 @@ def lib():
     L.cgpu_parse_mbufs.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp, vp]
     L.cgpu_group_by.restype = i32
     L.cgpu_group_by.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp]
+    L.cgpu_set_ip.restype = i32
+    L.cgpu_set_ip.argtypes = [vp, vp, ctypes.c_uint64, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp]
     if L.cgpu_abi_version() != ABI_VERSION:
         raise RuntimeError("capsule_amd: libcapsule_gpu.so ABI version mismatch")
     _lib = L

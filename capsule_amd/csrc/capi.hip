@@ -596,4 +596,28 @@ int cgpu_group_by(cgpu_ctx *ctx, const void *key, uint32_t key_kind, uint32_t n,
   return ok();
 }
 
+int cgpu_set_ip(cgpu_ctx *ctx, uint8_t *arena, uint64_t arena_len, const uint32_t *off,
+                const uint16_t *len, const uint32_t *meta, uint32_t n, const cgpu_ip_addr *src,
+                uint32_t src_stride, const cgpu_ip_addr *dst, uint32_t dst_stride,
+                uint8_t *status, void *stream) {
+  if (!ctx || n > CGPU_MAX_BATCH || src_stride > 1u || dst_stride > 1u) return fail(CGPU_EINVAL);
+  if (n == 0) return ok();
+  if (!arena || !off || !len || !meta || arena_len > 0xffff0000ull) return fail(CGPU_EINVAL);
+  cgpu::SetIpArgs a;
+  a.arena = arena;
+  a.arena_len = (uint32_t)arena_len;
+  a.off = off;
+  a.len = len;
+  a.meta = meta;
+  a.n = n;
+  a.src = src;
+  a.src_stride = src_stride;
+  a.dst = dst;
+  a.dst_stride = dst_stride;
+  a.status = status;
+  hipError_t e = cgpu::launch_set_ip(a, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e);
+  return ok();
+}
+
 }  // extern "C"

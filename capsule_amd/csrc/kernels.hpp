@@ -112,4 +112,20 @@ struct GroupByArgs {
 uint32_t group_by_tiles(uint32_t n);
 hipError_t launch_group_by(const GroupByArgs &a, hipStream_t s);
 
+// ---- set_src_ip / set_dst_ip (setip.hip) -----------------------------------
+struct SetIpArgs {
+  uint8_t *arena;
+  uint32_t arena_len;
+  const uint32_t *off;
+  const uint16_t *len;
+  const uint32_t *meta;
+  uint32_t n;
+  const cgpu_ip_addr *src;  // optional
+  uint32_t src_stride;
+  const cgpu_ip_addr *dst;  // optional
+  uint32_t dst_stride;
+  uint8_t *status;          // optional
+};
+hipError_t launch_set_ip(const SetIpArgs &a, hipStream_t s);
+
 }  // namespace cgpu

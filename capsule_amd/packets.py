@@ -303,6 +303,62 @@ def group_by(ctx, key, n_groups=None, by="key", idx=None, stream=None):
     return Groups(idx[:n], off)
 
 
+def ip_addrs(addrs):
+    """Host cgpu_ip_addr array from `ipaddress` objects (or (family, bytes))."""
+    a = np.zeros(len(addrs), np.dtype(N.IP_ADDR_FIELDS))
+    for i, x in enumerate(addrs):
+        fam, b = (x.version, x.packed) if hasattr(x, "packed") else x
+        if fam not in (4, 6) or len(b) != (4 if fam == 4 else 16):
+            raise ValueError(f"bad address {x!r}")
+        a[i]["family"] = fam
+        a[i]["octets"][: len(b)] = np.frombuffer(bytes(b), np.uint8)
+    return a
+
+
+def _addr_tensor(addrs, n, device):
+    if addrs is None:
+        return None, 0
+    if isinstance(addrs, np.ndarray):
+        addrs = torch.from_numpy(addrs.view(np.uint8).reshape(-1, N.IP_ADDR_SIZE)).to(device)
+    elif not isinstance(addrs, torch.Tensor):
+        addrs = torch.from_numpy(ip_addrs(addrs).view(np.uint8).reshape(-1, N.IP_ADDR_SIZE)).to(device)
+    if addrs.dtype != torch.uint8 or addrs.numel() % N.IP_ADDR_SIZE:
+        raise TypeError("addresses: cgpu_ip_addr records (uint8 [k, 20])")
+    k = addrs.numel() // N.IP_ADDR_SIZE
+    if k not in (1, n):
+        raise ValueError(f"{k} addresses for {n} packets (need 1 or n)")
+    return addrs.contiguous(), (0 if k == 1 else 1)
+
+
+def set_ip(ctx, batch, meta, src=None, dst=None, stream=None, status=None):
+    """`udp.set_src_ip(src)?; udp.set_dst_ip(dst)?` (udp.rs:174-201,
+    tcp.rs:432-459) for every packet the parse accepted as UDP/TCP, in place
+    in `batch.arena`: the address store plus the RFC 1624 incremental update
+    of the L4 checksum (checksum::compute_with_ipaddr, checksum.rs:202-220).
+    `src`/`dst`: one address for the whole burst or one per packet, as
+    `ipaddress` objects, a cgpu_ip_addr numpy array or a device uint8
+    [k, 20] tensor.  Returns the per-packet status (SETIP_*; a family
+    mismatch is the reference's "cannot mix IPv4 and IPv6 addresses.").
+    Asynchronous on `stream`."""
+    n = batch.n
+    dev = batch.arena.device
+    if meta.dtype != torch.int32 or meta.numel() != n:
+        raise TypeError("set_ip takes the int32 parse meta tensor of this batch")
+    s, ss = _addr_tensor(src, n, dev)
+    d, ds = _addr_tensor(dst, n, dev)
+    if status is None:
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
+    rc = N.lib().cgpu_set_ip(ctx.handle, _ptr(batch.arena), batch.arena.numel(), _ptr(batch.off),
+                             _ptr(batch.len), _ptr(meta), n, _ptr(s), ss, _ptr(d), ds,
+                             _ptr(status), _stream_handle(stream))
+    N.check(rc, "cgpu_set_ip")
+    if stream is not None:  # address copies made here must outlive the launch
+        for t in (s, d):
+            if t is not None:
+                t.record_stream(stream)
+    return status
+
+
 class Nat64Gateway:
     """examples/nat64 6to4 direction with its PORT_MAP on the device.
 

@@ -335,6 +335,37 @@ int cgpu_nat64_4to6(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in,
 int cgpu_group_by(cgpu_ctx *ctx, const void *key, uint32_t key_kind, uint32_t n,
                   uint32_t n_groups, uint32_t *idx, uint32_t *group_off, void *stream);
 
+/* ---- Udp/Tcp::set_src_ip / set_dst_ip (udp.rs:174-201, tcp.rs:432-459) ----
+ * Address rewrite with the incremental L4 checksum update, over a parsed
+ * batch (the bytes cgpu_parse_batch saw, its meta words).  For each packet
+ * whose meta is OK with a UDP or TCP layer (no extension header), in the
+ * order the reference's test calls them: if `src` is given,
+ * `set_src_ip(src[i * src_stride])`, then if `dst` is given,
+ * `set_dst_ip(dst[...])`.  Each is checksum::compute_with_ipaddr
+ * (checksum.rs:202-220: RFC 1624 `~(~HC + ~m + m')` over the 2 (v4) or 8
+ * (v6) address words of checksum.rs:182-195) on the stored checksum, then
+ * the address store, then Udp/Tcp::set_checksum (UDP stores 0 as 0xFFFF,
+ * udp.rs:132-141).  The IPv4 header checksum is left as it is, like
+ * Ipv4::set_src/set_dst (v4.rs:343-357).  An address of the other family
+ * fails that call with "cannot mix IPv4 and IPv6 addresses." and changes
+ * nothing (an earlier src update stays).  stride 0 broadcasts entry 0.
+ * status (optional, u8 per packet) = enum cgpu_setip_status.  The arena is
+ * updated in place; all device pointers; asynchronous on `stream`.         */
+typedef struct cgpu_ip_addr {
+  uint8_t octets[16]; /* wire order; IPv4 uses the first 4                  */
+  uint32_t family;    /* 4 or 6                                             */
+} cgpu_ip_addr;
+enum cgpu_setip_status {
+  CGPU_SETIP_OK = 0,
+  CGPU_SETIP_SKIPPED = 1,      /* meta not OK, or no UDP/TCP layer: untouched */
+  CGPU_SETIP_SRC_MISMATCH = 2, /* src family != packet's: untouched          */
+  CGPU_SETIP_DST_MISMATCH = 3, /* dst family != packet's: src (if any) applied */
+};
+int cgpu_set_ip(cgpu_ctx *ctx, uint8_t *arena, uint64_t arena_len, const uint32_t *off,
+                const uint16_t *len, const uint32_t *meta, uint32_t n, const cgpu_ip_addr *src,
+                uint32_t src_stride, const cgpu_ip_addr *dst, uint32_t dst_stride,
+                uint8_t *status, void *stream);
+
 /* ---- errors -------------------------------------------------------------- */
 int cgpu_last_error(void);
 const char *cgpu_strerror(int code);

@@ -766,3 +766,59 @@ void or_group_by(const void *key, uint32_t key_kind, uint32_t n, uint32_t n_grou
   free(cnt);
   free(cap);
 }
+
+/* ---- checksum.rs:202-220 `compute_with_ipaddr` --------------------------
+ * Returns 0 and the new checksum, or -1 for "cannot mix IPv4 and IPv6
+ * addresses." (:218).  Address words are Ipv4Addr -> u32 split hi/lo
+ * (:209-213) or Ipv6Addr::segments() (:215-216).                          */
+static int or_compute_with_ipaddr(uint16_t old_checksum, int old_v6, const uint8_t *old_addr,
+                                  const cgpu_ip_addr *new_addr, uint16_t *out) {
+  uint16_t ow[8], nw[8];
+  const size_t words = old_v6 ? 8 : 2;
+  if (new_addr->family != (old_v6 ? 6u : 4u)) return -1;
+  for (size_t i = 0; i < words; ++i) {
+    ow[i] = rd16(old_addr + 2 * i);
+    nw[i] = rd16(new_addr->octets + 2 * i);
+  }
+  *out = or_compute_inc(old_checksum, ow, nw, words);
+  return 0;
+}
+
+/* udp.rs:174-201 / tcp.rs:432-459 `set_src_ip` / `set_dst_ip`: checksum from
+ * the envelope's current address, then envelope_mut().set_src/set_dst
+ * (v4.rs:343-357 / v6/mod.rs:195-209: the field store only), then
+ * set_checksum (UDP: 0 stored as 0xFFFF, udp.rs:132-141; TCP as is).     */
+static int or_set_addr(uint8_t *frame, uint32_t l4_off, int udp, int v6, uint32_t addr_off,
+                       const cgpu_ip_addr *a) {
+  uint8_t *ck = frame + l4_off + (udp ? 6 : 16);
+  uint16_t c;
+  if (or_compute_with_ipaddr(rd16(ck), v6, frame + addr_off, a, &c) != 0) return -1;
+  memcpy(frame + addr_off, a->octets, v6 ? 16 : 4);
+  wr16(ck, (udp && c == 0) ? 0xFFFF : c);
+  return 0;
+}
+
+void or_set_ip(uint8_t *arena, const uint32_t *off, const uint16_t *len, const uint32_t *meta,
+               uint32_t n, const cgpu_ip_addr *src, uint32_t src_stride, const cgpu_ip_addr *dst,
+               uint32_t dst_stride, uint8_t *status) {
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t m = meta[i];
+    const uint32_t l3 = CGPU_META_L3(m), l4 = CGPU_META_L4(m), eth = CGPU_META_ETH_LEN(m);
+    const int udp = l4 == CGPU_L4_UDP, v6 = l3 == CGPU_L3_IPV6;
+    const uint32_t l4_off = eth + (v6 ? 40 : 20);
+    uint8_t st = CGPU_SETIP_OK;
+    if (CGPU_META_STATUS(m) != CGPU_PKT_OK || CGPU_META_EXT(m) != 0 || l3 == CGPU_L3_NONE ||
+        (l4 != CGPU_L4_UDP && l4 != CGPU_L4_TCP) || l4_off + (udp ? 8u : 20u) > len[i]) {
+      st = CGPU_SETIP_SKIPPED;
+    } else {
+      uint8_t *f = arena + off[i];
+      if (src && or_set_addr(f, l4_off, udp, v6, eth + (v6 ? 8 : 12),
+                             &src[(size_t)i * src_stride]) != 0)
+        st = CGPU_SETIP_SRC_MISMATCH;
+      else if (dst && or_set_addr(f, l4_off, udp, v6, eth + (v6 ? 24 : 16),
+                                  &dst[(size_t)i * dst_stride]) != 0)
+        st = CGPU_SETIP_DST_MISMATCH;
+    }
+    if (status) status[i] = st;
+  }
+}

@@ -75,6 +75,12 @@ void or_nat64_4to6(or_portmap *pm, const uint8_t *arena, const uint32_t *off, co
 void or_group_by(const void *key, uint32_t key_kind, uint32_t n, uint32_t n_groups, uint32_t *idx,
                  uint32_t *group_off);
 
+/* Udp/Tcp::set_src_ip then set_dst_ip (udp.rs:174-201, tcp.rs:432-459) on
+ * the packets or_parse_batch accepted as UDP/TCP; contract of cgpu_set_ip. */
+void or_set_ip(uint8_t *arena, const uint32_t *off, const uint16_t *len, const uint32_t *meta,
+               uint32_t n, const cgpu_ip_addr *src, uint32_t src_stride, const cgpu_ip_addr *dst,
+               uint32_t dst_stride, uint8_t *status);
+
 #ifdef __cplusplus
 }
 #endif

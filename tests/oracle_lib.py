@@ -56,6 +56,8 @@ def load(name="liboracle.so"):
     L.or_group_by.argtypes = [vp, u32, u32, u32, vp, vp]
     L.or_nat64_4to6.restype = None
     L.or_nat64_4to6.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
+    L.or_set_ip.restype = None
+    L.or_set_ip.argtypes = [vp, vp, vp, vp, u32, vp, u32, vp, u32, vp]
     return L
 
 
@@ -102,6 +104,34 @@ def parse_batch(arena, off, length, flags, fields=True):
     lib().or_parse_batch(_p(arena), _p(off), _p(length), n, flags, _p(meta), _p(csum), _p(h),
                          _p(fl))
     return meta, csum, h, fl
+
+
+IP_ADDR = np.dtype([("octets", "u1", (16,)), ("family", "<u4")])  # cgpu_ip_addr, 20 B
+
+
+def ip_addrs(addrs):
+    """[(family 4|6, bytes)] -> cgpu_ip_addr array."""
+    a = np.zeros(len(addrs), IP_ADDR)
+    for i, (fam, b) in enumerate(addrs):
+        a[i]["family"] = fam
+        a[i]["octets"][: len(b)] = np.frombuffer(bytes(b), np.uint8)
+    return a
+
+
+def set_ip(arena, off, length, meta, src=None, dst=None):
+    """Oracle Udp/Tcp::set_src_ip / set_dst_ip over a batch (arena copied) ->
+    (new arena, status u8[n]).  src/dst: cgpu_ip_addr arrays of length 1
+    (broadcast) or n."""
+    n = len(off)
+    out = np.array(arena, np.uint8, copy=True)
+    off = np.ascontiguousarray(off, np.uint32)
+    length = np.ascontiguousarray(length, np.uint16)
+    meta = np.ascontiguousarray(meta, np.uint32)
+    st = np.zeros(n, np.uint8)
+    ss = 0 if src is None or len(src) == 1 else 1
+    ds = 0 if dst is None or len(dst) == 1 else 1
+    lib().or_set_ip(_p(out), _p(off), _p(length), _p(meta), n, _p(src), ss, _p(dst), ds, _p(st))
+    return out, st
 
 
 def group_by(key, n_groups, kind=0):
