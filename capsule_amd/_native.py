@@ -50,6 +50,8 @@ ACT, DROP, ABORT = 0, 1, 2
 # rte_mbuf ingress (include/capsule_gpu.h; DPDK 19.11 field offsets)
 MBUF_BUF_ADDR_OFF, MBUF_DATA_OFF_OFF, MBUF_DATA_LEN_OFF, MBUF_SIZE = 0, 16, 40, 128
 INGRESS_STAGE, INGRESS_ZERO_COPY = 0, 1
+MBUF_PKT_LEN_OFF, MBUF_BUF_LEN_OFF = 36, 54
+NAT64_6TO4, NAT64_4TO6 = 0, 1
 
 KEY_U8, KEY_META_CLASS = 0, 1
 
@@ -124,7 +126,7 @@ EXPORTS = [
     "cgpu_portmap_create", "cgpu_portmap_destroy", "cgpu_portmap_next_port",
     "cgpu_portmap_size", "cgpu_nat64_6to4", "cgpu_nat64_4to6", "cgpu_group_by", "cgpu_last_error", "cgpu_strerror",
     "cgpu_pkt_status_str", "cgpu_abi_version", "cgpu_host_register", "cgpu_host_unregister",
-    "cgpu_parse_mbufs", "cgpu_set_ip",
+    "cgpu_parse_mbufs", "cgpu_set_ip", "cgpu_nat64_mbufs",
 ]
 
 _lib = None
@@ -176,6 +178,8 @@ def lib():
     L.cgpu_parse_mbufs.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp, vp]
     L.cgpu_group_by.restype = i32
     L.cgpu_group_by.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp]
+    L.cgpu_nat64_mbufs.restype = i32
+    L.cgpu_nat64_mbufs.argtypes = [vp, vp, u32, vp, u32, vp, vp]
     L.cgpu_set_ip.restype = i32
     L.cgpu_set_ip.argtypes = [vp, vp, ctypes.c_uint64, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp]
     if L.cgpu_abi_version() != ABI_VERSION:

@@ -44,6 +44,8 @@ struct cgpu_ctx {
   size_t arena_cap = 0;
   uint8_t *h_desc = nullptr, *d_desc = nullptr;  // off[n] | len[n] | outputs
   size_t desc_cap = 0;
+  uint8_t *d_out = nullptr;       // nat64 over mbufs: the rewritten frames
+  size_t out_cap = 0;
   uint32_t *gb_counts = nullptr;  // cgpu_group_by scratch
   size_t gb_cap = 0;              // entries
   // host regions registered for zero-copy ingress
@@ -136,6 +138,7 @@ void cgpu_ctx_destroy(cgpu_ctx *c) {
   if (c->h_desc) (void)hipHostFree(c->h_desc);
   if (c->d_desc) (void)hipFree(c->d_desc);
   if (c->gb_counts) (void)hipFree(c->gb_counts);
+  if (c->d_out) (void)hipFree(c->d_out);
   for (uint32_t r = 0; r < c->nreg; ++r)
     if (c->reg_owned[r]) (void)hipHostUnregister((void *)(uintptr_t)c->reg[r].host_base);
   (void)hipStreamDestroy(c->stream);
@@ -338,6 +341,9 @@ static int parse_zero_copy(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32
     g.len = (uint16_t *)(ctx->d_desc + lay.len);
     g.cursor = (uint32_t *)(ctx->d_desc + counters);
     g.bad = g.cursor + 1;
+    g.slot_extra = 0;
+    g.mb_dev = g.fr_dev = nullptr;
+    g.pkt_len = g.tailroom = nullptr;
     if (cgpu::launch_mbuf_gather(g, s) != hipSuccess) return fail(CGPU_EIO);
     if (int e = parse_and_return(ctx, ctx->d_arena, (size_t)m * kSlotMax + 64, m, lay, flags, meta,
                                  csum, flow_hash, fields, at))
@@ -560,6 +566,98 @@ int cgpu_nat64_4to6(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8
                     uint8_t *disposition, uint8_t *status, void *stream) {
   return nat64_call(false, ctx, pm, in, out_arena, out_arena_len, out_off, out_len, disposition,
                     status, stream);
+}
+
+// nat64 over an rte_mbuf burst: zero-copy gather, the device rewrite, the
+// ACT frames scattered back into their mbufs (cgpu_nat64_mbufs).
+static int nat64_mbufs(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, void *const *mbufs, uint32_t n,
+                       uint8_t *disposition, uint8_t *status) {
+  if (!ctx || !pm) return fail(CGPU_EINVAL);
+  if (n == 0) return ok();
+  if (!mbufs || !disposition || !status || ctx->nreg == 0) return fail(CGPU_EINVAL);
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
+  constexpr uint32_t kChunk = 1u << 20;
+  constexpr size_t kSlotMax = 2176;  // >= round_up(2048 + 20, 64)
+  const uint32_t m0 = n < kChunk ? n : kChunk;
+  const size_t arena_bytes = (size_t)m0 * kSlotMax + 64;
+  if (int e = grow(&ctx->h_arena, &ctx->d_arena, &ctx->arena_cap, arena_bytes)) return fail(e);
+  if (ctx->out_cap < arena_bytes) {
+    if (ctx->d_out) (void)hipFree(ctx->d_out);
+    ctx->d_out = nullptr;
+    ctx->out_cap = 0;
+    if (hipMalloc(&ctx->d_out, arena_bytes) != hipSuccess) return fail(CGPU_ENOMEM);
+    ctx->out_cap = arena_bytes;
+  }
+  // descriptor area: ptrs | off | len | out_len | disp | status | mb | fr | pkt_len | room | counters
+  const size_t o_ptr = 0, o_off = align_up(8ull * m0, 256), o_len = o_off + align_up(4ull * m0, 256);
+  const size_t o_olen = o_len + align_up(2ull * m0, 256), o_disp = o_olen + align_up(2ull * m0, 256);
+  const size_t o_st = o_disp + align_up(m0, 256), o_mb = o_st + align_up(m0, 256);
+  const size_t o_fr = o_mb + align_up(8ull * m0, 256), o_pl = o_fr + align_up(8ull * m0, 256);
+  const size_t o_tr = o_pl + align_up(4ull * m0, 256), o_cnt = o_tr + align_up(4ull * m0, 256);
+  if (int e = grow(&ctx->h_desc, &ctx->d_desc, &ctx->desc_cap, o_cnt + 256)) return fail(e);
+  uint8_t *D = ctx->d_desc, *H = ctx->h_desc;
+  hipStream_t s = ctx->stream;
+  uint32_t bad_total = 0;
+  for (uint32_t at = 0; at < n; at += m0) {
+    const uint32_t m = n - at < m0 ? n - at : m0;
+    memcpy(H + o_ptr, mbufs + at, 8ull * m);
+    if (hipMemcpyAsync(D + o_ptr, H + o_ptr, 8ull * m, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(D + o_cnt, 0, 8, s) != hipSuccess)
+      return fail(CGPU_EIO);
+    cgpu::GatherArgs g;
+    g.mbufs = (const uint64_t *)(D + o_ptr);
+    g.n = m;
+    g.nreg = ctx->nreg;
+    for (uint32_t r = 0; r < cgpu::kMaxRegions; ++r) g.reg[r] = ctx->reg[r];
+    g.arena = ctx->d_arena;
+    g.off = (uint32_t *)(D + o_off);
+    g.len = (uint16_t *)(D + o_len);
+    g.cursor = (uint32_t *)(D + o_cnt);
+    g.bad = g.cursor + 1;
+    g.slot_extra = to4 ? 0u : 20u;  // 4to6 frames grow by 20 B in their slot
+    g.mb_dev = (uint64_t *)(D + o_mb);
+    g.fr_dev = (uint64_t *)(D + o_fr);
+    g.pkt_len = (uint32_t *)(D + o_pl);
+    g.tailroom = (uint32_t *)(D + o_tr);
+    if (cgpu::launch_mbuf_gather(g, s) != hipSuccess) return fail(CGPU_EIO);
+    cgpu_batch in;
+    in.arena = ctx->d_arena;
+    in.arena_len = arena_bytes;
+    in.off = g.off;
+    in.len = g.len;
+    in.n = m;
+    if (int e = nat64_call(to4, ctx, pm, &in, ctx->d_out, arena_bytes, g.off, (uint16_t *)(D + o_olen),
+                           D + o_disp, D + o_st, s))
+      return e;
+    cgpu::ScatterArgs sc;
+    sc.out_arena = ctx->d_out;
+    sc.out_off = g.off;
+    sc.out_len = (const uint16_t *)(D + o_olen);
+    sc.disposition = D + o_disp;
+    sc.status = D + o_st;
+    sc.mb_dev = g.mb_dev;
+    sc.fr_dev = g.fr_dev;
+    sc.pkt_len = g.pkt_len;
+    sc.tailroom = g.tailroom;
+    sc.in_len = g.len;
+    sc.n = m;
+    sc.delta = to4 ? -20 : 20;
+    if (cgpu::launch_mbuf_scatter(sc, s) != hipSuccess) return fail(CGPU_EIO);
+    if (hipMemcpyAsync(H + o_disp, D + o_disp, o_mb - o_disp, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(H + o_cnt, D + o_cnt, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return fail(CGPU_EIO);
+    memcpy(disposition + at, H + o_disp, m);
+    memcpy(status + at, H + o_st, m);
+    bad_total += ((uint32_t *)(H + o_cnt))[1];
+  }
+  return bad_total ? fail(CGPU_EINVAL) : ok();
+}
+
+int cgpu_nat64_mbufs(cgpu_ctx *ctx, cgpu_portmap *pm, uint32_t direction, void *const *mbufs,
+                     uint32_t n, uint8_t *disposition, uint8_t *status) {
+  if (direction != CGPU_NAT64_6TO4 && direction != CGPU_NAT64_4TO6) return fail(CGPU_EINVAL);
+  return nat64_mbufs(direction == CGPU_NAT64_6TO4, ctx, pm, mbufs, n, disposition, status);
 }
 
 int cgpu_group_by(cgpu_ctx *ctx, const void *key, uint32_t key_kind, uint32_t n,

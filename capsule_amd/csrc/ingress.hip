@@ -70,20 +70,25 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
     const uint64_t dmm = __shfl(dm, (int)m);
     const bool okm = __shfl((int)mok, (int)m) != 0;
     H[r] = u32x4{0u, 0u, 0u, 0u};
-    if (okm && q < 3u) H[r] = *reinterpret_cast<const u32x4 *>(dmm + 16u * q);
+    // bytes 48..63 (buf_len @54) only for the egress path
+    if (okm && (q < 3u || g.tailroom)) H[r] = *reinterpret_cast<const u32x4 *>(dmm + 16u * q);
   }
   const uint32_t r_own = lane >> 4, src_lane = 4u * (lane & 15u);
-  uint32_t ba_lo = 0, ba_hi = 0, doff = 0, dlen = 0;
+  uint32_t ba_lo = 0, ba_hi = 0, doff = 0, dlen = 0, plen = 0, blen = 0;
 #pragma unroll
   for (uint32_t r = 0; r < 4u; ++r) {
     const uint32_t lo = __shfl(H[r][0], (int)src_lane), hi = __shfl(H[r][1], (int)src_lane);
     const uint32_t d16 = __shfl(H[r][0], (int)(src_lane + 1u));  // bytes 16..19
     const uint32_t d40 = __shfl(H[r][2], (int)(src_lane + 2u));  // bytes 40..43
+    const uint32_t d36 = __shfl(H[r][1], (int)(src_lane + 2u));  // bytes 36..39
+    const uint32_t d52 = __shfl(H[r][1], (int)(src_lane + 3u));  // bytes 52..55
     if (r == r_own) {
       ba_lo = lo;
       ba_hi = hi;
       doff = d16 & 0xffffu;
       dlen = d40 & 0xffffu;
+      plen = d36;
+      blen = d52 >> 16;
     }
   }
   uint64_t src = 0;
@@ -95,8 +100,14 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
     L = ok ? dlen : 0u;
     if (!ok) atomicAdd(g.bad, 1u);
   }
+  if (valid && g.mb_dev) {
+    g.mb_dev[i] = ok ? dm : 0ull;
+    g.fr_dev[i] = src;
+    g.pkt_len[i] = plen;
+    g.tailroom[i] = (blen - doff - dlen) & 0xffffu;  // u16 arithmetic, as Mbuf::tailroom
+  }
   // --- slots: one atomic per wave, prefix within the wave ---------------------
-  const uint32_t slot = (L + 63u) & ~63u;
+  const uint32_t slot = (L + g.slot_extra + 63u) & ~63u;
   uint32_t incl = slot;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -140,7 +151,60 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
   }
 }
 
+// Egress for nat64 over mbufs: every ACT frame back into its own mbuf, at
+// buf_addr + data_off (Mbuf::shrink / extend move bytes, never data_off,
+// mbuf.rs:225-270), and data_len / pkt_len adjusted by the same delta.  4to6
+// first applies extend's tailroom check (`20 < tailroom`, mbuf.rs:228) with
+// the mbuf's real buf_len: a frame without the room is ABORT / NOT_RESIZED
+// and its mbuf is left as it was.  16-lane groups write four frames per
+// round, 16 B per lane, as posted PCIe writes to the registered mempool.
+__global__ __launch_bounds__(kBlock) void mbuf_scatter(ScatterArgs a) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  bool act = false;
+  uint32_t nl = 0;
+  if (i < a.n && a.disposition[i] == CGPU_ACT && a.mb_dev[i] != 0ull) {
+    act = true;
+    if (a.delta > 0 && !((uint32_t)a.delta < a.tailroom[i])) {
+      act = false;
+      a.disposition[i] = CGPU_ABORT;
+      a.status[i] = CGPU_PKT_NOT_RESIZED;
+    } else {
+      nl = a.out_len[i];
+      uint8_t *h = reinterpret_cast<uint8_t *>(a.mb_dev[i]);
+      *reinterpret_cast<uint16_t *>(h + CGPU_MBUF_DATA_LEN_OFF) = (uint16_t)nl;
+      *reinterpret_cast<uint32_t *>(h + CGPU_MBUF_PKT_LEN_OFF) = a.pkt_len[i] + (uint32_t)a.delta;
+    }
+  }
+  const uint32_t o = act ? a.out_off[i] : 0u;
+  const uint64_t dst = act ? a.fr_dev[i] : 0ull;
+  const uint32_t grp = lane >> 4, gl = lane & 15u;
+  for (uint32_t r = 0; r < 16u; ++r) {
+    const uint32_t f = 4u * r + grp;
+    const uint32_t fl = __shfl(nl, (int)f);
+    if (!__ballot(fl != 0u)) continue;
+    const uint64_t fd = __shfl(dst, (int)f);
+    const uint32_t fo = __shfl(o, (int)f);
+    for (uint32_t pos = 16u * gl; pos < fl; pos += 256u) {
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(a.out_arena + fo + pos);
+      uint8_t *p = reinterpret_cast<uint8_t *>(fd + pos);
+      const uint32_t r16 = fl - pos;
+      if (((fd + pos) & 15u) == 0u && r16 >= 16u) {
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+      } else {
+        for (uint32_t b = 0; b < 16u && b < r16; ++b) p[b] = (uint8_t)(v[b >> 2] >> (8u * (b & 3u)));
+      }
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_mbuf_scatter(const ScatterArgs &a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mbuf_scatter, dim3((a.n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_mbuf_gather(const GatherArgs &g, hipStream_t s) {
   if (g.n == 0) return hipSuccess;

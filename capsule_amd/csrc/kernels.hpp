@@ -94,8 +94,31 @@ struct GatherArgs {
   uint16_t *len;          // [n]
   uint32_t *cursor;       // slot allocation cursor (zero before the launch)
   uint32_t *bad;          // mbufs / frames outside every registered region
+  uint32_t slot_extra;    // bytes of room past each frame in its slot (nat64 4to6: 20)
+  // optional (nullptr: not written), for the egress scatter:
+  uint64_t *mb_dev;       // [n] device address of the rte_mbuf header (0: bad)
+  uint64_t *fr_dev;       // [n] device address of the frame (buf_addr + data_off)
+  uint32_t *pkt_len;      // [n] rte_mbuf pkt_len (@36)
+  uint32_t *tailroom;     // [n] buf_len - data_off - data_len (Mbuf::tailroom, mbuf.rs:207-213)
 };
 hipError_t launch_mbuf_gather(const GatherArgs &g, hipStream_t s);
+
+// Egress: the rewritten ACT frames back into their own mbufs.
+struct ScatterArgs {
+  const uint8_t *out_arena;
+  const uint32_t *out_off;
+  const uint16_t *out_len;
+  uint8_t *disposition;   // ACT frames are written; 4to6 without tailroom -> ABORT
+  uint8_t *status;
+  const uint64_t *mb_dev;
+  const uint64_t *fr_dev;
+  const uint32_t *pkt_len;
+  const uint32_t *tailroom;
+  const uint16_t *in_len;
+  uint32_t n;
+  int32_t delta;          // data_len change: -20 (6to4) or +20 (4to6)
+};
+hipError_t launch_mbuf_scatter(const ScatterArgs &a, hipStream_t s);
 
 // ---- group_by --------------------------------------------------------------
 struct GroupByArgs {

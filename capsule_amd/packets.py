@@ -421,6 +421,22 @@ class Nat64Gateway:
         return self._call(N.lib().cgpu_nat64_4to6, "cgpu_nat64_4to6", 20, batch, out_arena,
                           out_off, stream, out)
 
+    def nat_mbufs(self, mbufs, direction="6to4"):
+        """`install_6to4` / `install_4to6` (examples/nat64/main.rs:152-165)
+        on a burst of rte_mbufs (u64 numpy array of their addresses, from a
+        mempool registered with HostRegion): the device reads the frames,
+        rewrites them and writes every ACT frame back into its own mbuf
+        (data_len / pkt_len -20 or +20).  Returns host (disposition, status)."""
+        mbufs = np.ascontiguousarray(mbufs, dtype=np.uint64)
+        n = len(mbufs)
+        disp = np.zeros(n, np.uint8)
+        st = np.zeros(n, np.uint8)
+        d = {"6to4": N.NAT64_6TO4, "4to6": N.NAT64_4TO6}[direction]
+        rc = N.lib().cgpu_nat64_mbufs(self.ctx.handle, self._h, d, mbufs.ctypes.data, n,
+                                      disp.ctypes.data, st.ctypes.data)
+        N.check(rc, "cgpu_nat64_mbufs")
+        return disp, st
+
     def close(self):
         if self._h:
             N.lib().cgpu_portmap_destroy(self._h)

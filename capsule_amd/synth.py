@@ -364,17 +364,20 @@ def nat64_replies(out_arena, off, out_len):
     return a, off.astype(np.uint32), out_len.astype(np.uint16)
 
 
-def mbuf_pool(arena, off, length, mem=None, headroom=128, seed=7):
+def mbuf_pool(arena, off, length, mem=None, headroom=128, seed=7, room=None):
     """Lay a batch out as a DPDK-style mempool in host memory: one object per
-    packet = a 128-B rte_mbuf header (buf_addr @0, data_off @16, data_len
-    @40; DPDK 19.11 offsets) followed by its buffer (headroom + frame), object
-    stride a multiple of 64, objects in shuffled order (a pool hands out
-    buffers in no particular order).  `mem`: a u8 array to build in (e.g. a
-    pinned torch tensor's numpy view), else a new numpy array.  Returns
-    (mem, mbufs u64[n] = the rte_mbuf addresses in batch order)."""
+    packet = a 128-B rte_mbuf header (buf_addr @0, data_off @16, pkt_len @36,
+    data_len @40, buf_len @54; DPDK 19.11 offsets) followed by its buffer
+    (headroom + a data room of `room` bytes, default the longest frame; DPDK's
+    default is 2048), object stride a multiple of 64, objects in shuffled
+    order (a pool hands out buffers in no particular order).  `mem`: a u8
+    array to build in (e.g. a pinned torch tensor's numpy view), else a new
+    numpy array.  Returns (mem, mbufs u64[n] = the rte_mbuf addresses in
+    batch order)."""
     n = len(off)
     length = np.asarray(length, dtype=np.int64)
-    room = int(length.max()) if n else 0
+    if room is None:
+        room = int(length.max()) if n else 0
     stride = (128 + headroom + room + 63) // 64 * 64
     need = max(stride * n, 64)
     if mem is None:
@@ -390,6 +393,11 @@ def mbuf_pool(arena, off, length, mem=None, headroom=128, seed=7):
     mem[objs + 17] = headroom >> 8
     mem[objs + 40] = (length & 0xFF).astype(np.uint8)
     mem[objs + 41] = (length >> 8).astype(np.uint8)
+    for b in range(4):  # pkt_len = data_len (one segment)
+        mem[objs + 36 + b] = ((length >> (8 * b)) & 0xFF).astype(np.uint8)
+    buf_len = headroom + room
+    mem[objs + 54] = buf_len & 0xFF
+    mem[objs + 55] = buf_len >> 8
     src0 = np.asarray(off, dtype=np.int64)
     dst0 = objs + 128 + headroom
     for c in range(0, n, 1 << 16):  # frames, 64 Ki packets at a time

@@ -315,6 +315,27 @@ int cgpu_nat64_4to6(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in,
                     uint8_t *out_arena, uint64_t out_arena_len, const uint32_t *out_off,
                     uint16_t *out_len, uint8_t *disposition, uint8_t *status, void *stream);
 
+/* ---- nat64 over an rte_mbuf burst (the DPDK seam, both directions) -------
+ * install_6to4 / install_4to6 (examples/nat64/main.rs:152-165) applied to a
+ * burst exactly as PacketRx::receive returns it (an array of rte_mbuf*): the
+ * device reads the frames from the registered mempool (cgpu_host_register,
+ * zero-copy), rewrites them as cgpu_nat64_6to4 / cgpu_nat64_4to6, and writes
+ * every ACT frame back into its own mbuf over PCIe: the new frame at
+ * buf_addr + data_off (Mbuf::shrink / extend move bytes, never data_off,
+ * mbuf.rs:225-270), data_len and pkt_len changed by -20 (6to4) / +20 (4to6).
+ * 4to6 checks extend's `20 < tailroom` (mbuf.rs:228) against the mbuf's own
+ * buf_len (@54); without the room the packet is ABORT / NOT_RESIZED.  DROP
+ * and ABORT mbufs are not touched: the caller frees or forwards them
+ * (Send::run, batch/send.rs:95-118).  disposition / status: HOST arrays [n].
+ * Synchronous.  Fails with CGPU_EINVAL if a pointer lies outside every
+ * registered region (nothing is read or written through it).             */
+#define CGPU_NAT64_6TO4 0u
+#define CGPU_NAT64_4TO6 1u
+#define CGPU_MBUF_PKT_LEN_OFF 36
+#define CGPU_MBUF_BUF_LEN_OFF 54
+int cgpu_nat64_mbufs(cgpu_ctx *ctx, cgpu_portmap *pm, uint32_t direction, void *const *mbufs,
+                     uint32_t n, uint8_t *disposition, uint8_t *status);
+
 /* ---- group_by (core/src/batch/group_by.rs:143-172) -----------------------
  * Stable partition of a batch's packet indices by a per-packet arm key: the
  * device form of `batch.group_by(selector, compose!{...})`.  Arm k (k <

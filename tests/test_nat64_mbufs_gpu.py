@@ -1,0 +1,121 @@
+"""examples/nat64 over rte_mbuf bursts (cgpu_nat64_mbufs, the DPDK seam of
+SURVEY §8 f2 with egress): the device reads the frames from a registered
+DPDK-style mempool, rewrites them and writes every ACT frame back into its own
+mbuf.  Checked bit-exactly against the oracle's nat_6to4 / nat_4to6 on the
+same frames: dispositions, statuses, and for every mbuf its data_len, pkt_len
+and frame bytes (Mbuf::shrink / extend keep data_off, mbuf.rs:225-270);
+DROP / ABORT mbufs must be untouched."""
+import numpy as np
+import pytest
+
+import oracle_lib
+from capsule_amd import _native as N
+from capsule_amd import packets, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _u16(mem, at):
+    return mem[at].astype(np.int64) | (mem[at + 1].astype(np.int64) << 8)
+
+
+def _u32(mem, at):
+    return sum(mem[at + b].astype(np.int64) << (8 * b) for b in range(4))
+
+
+def _check_mbufs(mem, mbufs, a, o, l, out, out_off, olen, disp):
+    """Every mbuf against the oracle: ACT -> the rewritten frame, else untouched."""
+    objs = (mbufs - np.uint64(mem.ctypes.data)).astype(np.int64)
+    dlen, plen = _u16(mem, objs + 40), _u32(mem, objs + 36)
+    doff = _u16(mem, objs + 16)
+    data = objs + 128 + doff
+    act = disp == N.ACT
+    want = np.where(act, olen.astype(np.int64), l.astype(np.int64))
+    assert (dlen == want).all(), np.nonzero(dlen != want)[0][:8]
+    assert (plen == want).all()
+    for i in range(len(mbufs)):
+        d, L = int(data[i]), int(want[i])
+        if act[i]:
+            s = int(out_off[i])
+            assert (mem[d : d + L] == out[s : s + L]).all(), f"frame {i}"
+        else:
+            s = int(o[i])
+            assert (mem[d : d + L] == a[s : s + L]).all(), f"untouched frame {i}"
+
+
+def _pool(ctx, a, o, l, room):
+    mem, mbufs = synth.mbuf_pool(a, o, l, room=room)
+    return mem, mbufs, packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+
+
+def test_nat64_mbufs_6to4_then_4to6_replies(ctx):
+    a, o, l = synth.nat64_stream(20_000, n_keys=3000, drop_frac=0.05, seed=41)
+    mem, mbufs, reg = _pool(ctx, a, o, l, 2048)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=14)
+    pm = oracle_lib.PortMap()
+    try:
+        disp, st = gw.nat_mbufs(mbufs, "6to4")
+        out, olen, odisp, ost = pm.nat_6to4(a, o, l)
+        assert (disp == odisp).all() and (st == ost).all()
+        assert (odisp == N.ACT).sum() > 15_000 and (odisp != N.ACT).any()
+        _check_mbufs(mem, mbufs, a, o, l, out, o, olen, disp)
+        assert gw.next_port() == pm.next_port()
+    finally:
+        reg.close()
+
+    keep = np.nonzero(odisp == N.ACT)[0]
+    ra, ro, rl = synth.nat64_replies(out, o[keep], olen[keep])
+    mem2, mb2, reg2 = _pool(ctx, ra, ro, rl, 2048)
+    try:
+        disp6, st6 = gw.nat_mbufs(mb2, "4to6")
+        out6, olen6, odisp6, ost6 = pm.nat_4to6(ra, ro, rl, ro, len(ra))
+        assert (disp6 == odisp6).all() and (st6 == ost6).all() and (odisp6 == N.ACT).all()
+        _check_mbufs(mem2, mb2, ra, ro, rl, out6, ro, olen6, disp6)
+    finally:
+        reg2.close()
+        gw.close()
+
+
+@pytest.mark.parametrize("extra", [20, 21])
+def test_nat64_mbufs_4to6_tailroom(ctx, extra):
+    """extend(20) needs 20 < tailroom (mbuf.rs:228): with exactly 20 bytes of
+    room every reply is ABORT / NOT_RESIZED and its mbuf untouched; with 21
+    every reply is rewritten."""
+    a, o, l = synth.nat64_stream(2_000, n_keys=200, drop_frac=0.0, seed=42)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=12)
+    pm = oracle_lib.PortMap()
+    b = packets.PacketBatch.from_numpy(a, o, l, "cuda:0")
+    gw.nat_6to4(b)  # populate the port map (the device and the oracle alike)
+    out, olen, odisp, _ = pm.nat_6to4(a, o, l)
+    keep = np.nonzero(odisp == N.ACT)[0]
+    ra, ro, rl = synth.nat64_replies(out, o[keep], olen[keep])
+    room = int(rl.max()) + extra
+    assert (rl == rl.max()).all()
+    mem, mbufs, reg = _pool(ctx, ra, ro, rl, room)
+    try:
+        disp, st = gw.nat_mbufs(mbufs, "4to6")
+        out6, olen6, odisp6, ost6 = pm.nat_4to6(ra, ro, rl, ro, len(ra))
+        if extra <= 20:
+            assert (disp == N.ABORT).all() and (st == N.PKT["NOT_RESIZED"]).all()
+        else:
+            assert (disp == odisp6).all() and (st == ost6).all() and (disp == N.ACT).all()
+        _check_mbufs(mem, mbufs, ra, ro, rl, out6, ro, olen6, disp)
+    finally:
+        reg.close()
+        gw.close()
+
+
+def test_nat64_mbufs_rejects_unregistered_and_empty(ctx):
+    gw = packets.Nat64Gateway(ctx, capacity_log2=8)
+    a, o, l = synth.nat64_stream(64, n_keys=8, seed=43)
+    mem, mbufs, reg = _pool(ctx, a, o, l, 2048)
+    try:
+        d, s = gw.nat_mbufs(mbufs[:0], "6to4")
+        assert d.size == 0
+        bad = mbufs.copy()
+        bad[5] = np.uint64(0x1000)  # outside every registered region
+        with pytest.raises(N.CgpuError):
+            gw.nat_mbufs(bad, "6to4")
+    finally:
+        reg.close()
+        gw.close()
