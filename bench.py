@@ -1,6 +1,6 @@
 """Device-resident packet-path benchmark (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config parse64|imix|imix_csum|nat64]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config parse64|...] [--only]
 
 A step is one pass of the hot path over one batch of synthetic packets that
 is already resident in HBM.  Default workload = BASELINE config 2 with the
@@ -8,17 +8,29 @@ north-star feature set: 1,048,576 x 64-B Ethernet/IPv4/UDP frames, parse +
 IPv4 header checksum + UDP checksum verify + 5-tuple flow hash, one
 `cgpu_parse_batch` launch per step.  To keep the measurement an HBM one, each
 rank keeps R copies of its batch at different HBM addresses (R x 70 MB >
-the 256 MiB Infinity Cache) and step k processes copy k mod R.
+the 256 MiB Infinity Cache) and step k processes copy k mod R.  Every timed
+region follows at least W warm-up launches and MIN_WARM_S of device time.
 
-Multi-GPU (torch.distributed.run, one process per GPU): every rank owns an
-independent RX-queue shard (its own seed, its own HBM) -- no data-path
-collective, weak scaling; the process group only carries the barriers and the
-max-over-ranks of the elapsed time.  value = packets processed by all ranks /
-that time.
+Multi-GPU: one process per GPU, either started by torch.distributed.run or,
+when `--gpus N` > 1 arrives without WORLD_SIZE in the environment, by this
+script's own launcher (shards.launch_ranks: N child processes; the parent
+never touches the GPU).  Every rank owns an independent RX-queue shard (its
+own seed, its own HBM) -- no data-path collective, no RCCL, weak scaling;
+a gloo process group carries only the barriers, the max-over-ranks of the
+elapsed time and the per-rank figures.  value = packets processed by all
+ranks / that time.
 
-Rank 0 prints ONE JSON line with `roofline` (dominant kernel, per-launch HIP
-event timing on the launch stream) and, at N=1, `cpu_baseline` (the C oracle
-restatement of the same workload timed on a bounded sample on one host core).
+Rank 0 prints ONE JSON line:
+  value / roofline    the --config (default parse64) on every rank; roofline
+                      per launch from HIP events on the launch stream, with
+                      each rank's fraction in roofline.per_rank;
+  shards              BASELINE config 5: IMIX parse + hash, one shard per GPU,
+                      aggregate Mpps and per-rank roofline fraction (every N);
+  sizes               N=1 only: the metric's other frame sizes (256 B, 1500 B)
+                      and configs 3, 3' and 4 (IMIX, IMIX + checksums, nat64),
+                      each with its own warm-up and timed loop;
+  cpu_baseline        N=1 only: the C oracle restatement of the same workload
+                      on a bounded sample, one host core and one per shard.
 """
 import argparse
 import ctypes
@@ -199,6 +211,29 @@ def cpu_baseline(w, seconds):
             passes += 1
         el = time.perf_counter() - t0
         res["multi_parse_udp_mpps"] = round(passes * n / el / 1e6, 3)
+        # ... and on the reference bench's own input shape: v4_udp() builds
+        # 42-B header-only Eth/IPv4/UDP packets (testils/proptest/strategy.rs:
+        # 446-448), each in its own mbuf (128-B rte_mbuf + 128-B headroom,
+        # 2304-B objects), parsed in batches of 500 (bench/packets.rs:31).
+        from capsule_amd import synth
+
+        m, stride = 500 * 64, 2304
+        frames = synth.build_frames(np.random.default_rng(7), m, synth.V4_UDP, 42)
+        a42 = np.zeros(m * stride, np.uint8)
+        a42.reshape(m, stride)[:, 256:298] = frames
+        o42 = (np.arange(m, dtype=np.uint32) * stride + 256).astype(np.uint32)
+        l42 = np.full(m, 42, np.uint16)
+        assert L.or_multi_parse_udp(p(a42), p(o42), p(l42), m) == m
+        passes, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < min(3.0, seconds):
+            for s in range(0, m, 500):
+                L.or_multi_parse_udp(p(a42), p(o42[s:s + 500]), p(l42[s:s + 500]), 500)
+            passes += 1
+        el = time.perf_counter() - t0
+        res["multi_parse_udp_42B"] = {
+            "value": round(passes * m / el / 1e6, 3), "unit": "Mpps", "cores": 1,
+            "sample": f"{m} 42-B v4_udp() packets in 2304-B mbuf objects, batches of 500, "
+                      f"{passes} passes, {el:.1f} s"}
     try:
         res["host_cpu"] = next(x.split(":", 1)[1].strip() for x in
                                open("/proc/cpuinfo") if x.startswith("model name"))
@@ -207,21 +242,206 @@ def cpu_baseline(w, seconds):
     return res
 
 
+SEEDS = {"parse64": 2, "parse256": 2, "parse1500": 2, "imix": 3, "imix_csum": 3, "nat64": 4,
+         "nat64_4to6": 4}
+CONFIGS = tuple(SEEDS)
+METRIC = "Mpps device-resident parse+cksum+hash @64/256/1500B; % HBM-read roofline"
+# the metric's other sizes and BASELINE's other single-GPU configs, timed in
+# the same N=1 run (the `sizes` object of the line)
+SIZES = ("parse256", "parse1500", "imix", "imix_csum", "nat64")
+# BASELINE config 5: IMIX shards, one per GPU (the `shards` object)
+SHARD_CONFIG = "imix"
+MIN_WARM_S = 0.06  # device time of warm-up before any timed region (steady clocks)
+
+
+def pmc_traffic(cfg):
+    """HBM bytes per launch from profiles/pmc_<cfg>.json, when that profile
+    was taken on the current kernel sources (scripts/summarize_prof.py)."""
+    pmc = ROOT / "profiles" / f"pmc_{cfg}.json"
+    if not pmc.exists():
+        return None
+    sys.path.insert(0, str(ROOT / "scripts"))
+    from summarize_prof import source_hash
+
+    p = json.loads(pmc.read_text())
+    if p.get("src_hash") == source_hash(cfg) and "traffic_bytes" in p:
+        return int(p["traffic_bytes"])
+    return None
+
+
+def bench_config(cfg, g, ctx, dev, steps, warmup, w=None):
+    """Time one config on this rank.
+
+    Builds the rank's shard of the workload, keeps R copies resident in HBM
+    (R x batch > 2 x the 256 MiB Infinity Cache; launch k processes copy
+    k mod R), warms up for at least `warmup` launches AND MIN_WARM_S of
+    device time, then times `steps` launches between a sync + barrier on
+    each side (ShardGroup.timed: max over ranks).  HIP events recorded on the
+    launch stream around the same launches give the per-launch device time.
+    """
+    import torch
+
+    from capsule_amd import packets
+
+    w = w or make_workload(cfg, g.shard_seed(0xC0FFEE + SEEDS[cfg]))
+    n = len(w["off"])
+    gw = nat64_4to6_setup(w, ctx, dev) if w["kind"] == "nat64_4to6" else None
+    batch_bytes = len(w["arena"]) + 6 * n
+    copies = max(2, -(-2 * INFINITY_CACHE // batch_bytes))
+    b0 = packets.PacketBatch.from_numpy(w["arena"], w["off"], w["len"], dev)
+    batches = [b0] + [packets.PacketBatch(b0.arena.clone(), b0.off.clone(), b0.len.clone())
+                      for _ in range(copies - 1)]
+    stream = torch.cuda.current_stream(dev)
+    if w["kind"] == "parse":
+        # checksum verify: CSUM_OK bits in meta, computed values not stored
+        outs = [packets.ParseBuffers(n, dev, csum=False) for _ in range(2)]
+        launchers = [packets.ParseLauncher(ctx, batches[k % copies], outs[k & 1], w["flags"],
+                                           stream) for k in range(2 * copies)]
+    else:
+        direction = "4to6" if gw is not None else "6to4"
+        gw = gw or packets.Nat64Gateway(ctx, capacity_log2=17)
+        outs = [(torch.empty_like(b.arena), b.off, torch.empty(n, dtype=torch.int16, device=dev),
+                 torch.empty(n, dtype=torch.uint8, device=dev),
+                 torch.empty(n, dtype=torch.uint8, device=dev)) for b in batches[:2]]
+        launchers = [packets.Nat64Launcher(gw, batches[k % copies], outs[k & 1], stream,
+                                           direction) for k in range(2 * copies)]
+    cycle = len(launchers)
+
+    # warm-up: >= `warmup` launches and >= MIN_WARM_S of device time
+    k = 0
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    while k < warmup or time.perf_counter() - t0 < MIN_WARM_S:
+        for _ in range(16):
+            launchers[k % cycle]()
+            k += 1
+        torch.cuda.synchronize(dev)
+
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    state = {"k": k, "left": steps}
+
+    def one():
+        if state["left"] == steps:
+            ev0.record(stream)
+        launchers[state["k"] % cycle]()
+        state["k"] += 1
+        state["left"] -= 1
+        if state["left"] == 0:
+            ev1.record(stream)
+
+    elapsed = g.timed(one, steps, sync=lambda: torch.cuda.synchronize(dev))
+    kern_us = ev0.elapsed_time(ev1) / steps * 1e3
+    res = dict(cfg=cfg, n=n, desc=w["desc"], frame=w["frame"], copies=copies, elapsed=elapsed,
+               steps=steps, kern_us=kern_us, algo_bytes=w["algo_bytes"],
+               achieved=w["algo_bytes"] / (kern_us * 1e-6) / 1e9, w=w)
+    del launchers, outs, batches, b0
+    if gw is not None:
+        gw.close()
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    return res
+
+
+def summarize(r, g):
+    """Aggregate of one config over the ranks (collective: every rank calls
+    it in the same order)."""
+    fr = g.gather(r["achieved"] / HBM_PEAK_GBS)
+    us = g.gather(r["kern_us"])
+    total = g.sum(r["n"] * r["steps"])
+    return {
+        "workload": r["desc"], "packets_per_step": r["n"], "steps": r["steps"],
+        "mpps": round(total / r["elapsed"] / 1e6, 2),
+        "ms_per_step": round(r["elapsed"] / r["steps"] * 1e3, 5),
+        "kernel_us": round(r["kern_us"], 3),
+        "achieved_GBps": round(r["achieved"], 1),
+        "frac": round(r["achieved"] / HBM_PEAK_GBS, 4),
+        "algo_bytes_per_launch": r["algo_bytes"],
+        "traffic": r["traffic"] if "traffic" in r else pmc_traffic(r["cfg"]),
+        "per_rank": [{"rank": i, "kernel_us": round(u, 3), "frac": round(f, 4)}
+                     for i, (u, f) in enumerate(zip(us, fr))],
+    }
+
+
+def stub_worker(args):
+    """GPU-free stand-in for one rank (--stub, for CPU tests of the launcher
+    and of the line's shape): the same ShardGroup control plane and the same
+    JSON line, with a sleep in place of each launch."""
+    from capsule_amd.shards import ShardGroup
+
+    g = ShardGroup()
+
+    def fake(cfg, steps):
+        el = g.timed(lambda: time.sleep(1e-4 * (1 + g.rank)), steps)
+        return dict(cfg=cfg, n=1 << 20, desc=f"stub {cfg}", frame="-", copies=0, elapsed=el,
+                    steps=steps, kern_us=100.0 * (1 + g.rank), algo_bytes=70 << 20,
+                    achieved=(70 << 20) / (1e-4 * (1 + g.rank)) / 1e9, w=None, traffic=None)
+
+    main = fake(args.config, args.steps)
+    extra = {} if args.only else {"shards": dict(summarize(fake(SHARD_CONFIG, args.steps), g),
+                                                  config=SHARD_CONFIG)}
+    if not args.only and g.world == 1:
+        extra["sizes"] = {c: summarize(fake(c, args.steps), g) for c in SIZES}
+    emit(args, g, main, extra, stub=True)
+    g.close()
+
+
+def emit(args, g, m, extra, cpu=None, stub=False):
+    s = summarize(m, g)
+    total = g.sum(m["n"] * m["steps"])
+    result = {
+        "metric": METRIC,
+        "value": round(total / m["elapsed"] / 1e6, 2),
+        "unit": "Mpps",
+        "n_gpus": g.world,
+        "steps": m["steps"],
+        "warmup": args.warmup,
+        "ms_per_step": round(m["elapsed"] / m["steps"] * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded proptest-style reconciled frames, one shard per rank)",
+        "config": {"workload": m["desc"], "config": m["cfg"], "packets_per_step": m["n"],
+                   "global_batch": m["n"] * g.world, "resident_copies": m["copies"],
+                   "launch": "direct",
+                   "parallelism": f"{g.world} independent RX-queue shards, one per GPU "
+                                  "(no collective; gloo control plane only)"},
+        "roofline": {"bound": "hbm", "achieved": s["achieved_GBps"], "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": s["frac"], "traffic": s["traffic"],
+                     "kernel_us": s["kernel_us"], "algo_bytes_per_launch": m["algo_bytes"],
+                     "per_rank": s["per_rank"],
+                     "mean_frac_over_ranks": round(sum(r["frac"] for r in s["per_rank"]) /
+                                                   g.world, 4)},
+        "parity": {"parse_and_checksums": "bit-exact vs the C oracle, which is pinned by the "
+                                          "reference's own KATs (tests/golden)",
+                   "flow_hash": "bit-exact vs the C oracle; parity unpinned vs the reference "
+                                "(convention: SipHash-1-3(0,0) over Rust-1.50 derive(Hash) "
+                                "of Flow, no reference vector exists)",
+                   "nat64_bytes": "bit-exact vs the C oracle; parity unpinned vs the reference "
+                                  "(examples/nat64 has no test or expected output)"},
+    }
+    result.update(extra)
+    if cpu is not None:
+        result["cpu_baseline"] = cpu
+    if stub:
+        result["stub"] = True
+    if g.rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # ~40 ms of warmup brings the GPU to its steady clocks: with 50 warmup
-    # steps the 64-B config measured 18.5 us per launch, with 2000 17.2 us.
-    ap.add_argument("--steps", type=int, default=5000)
-    ap.add_argument("--warmup", type=int, default=2000)
-    ap.add_argument("--config", default="parse64",
-                    choices=["parse64", "parse256", "parse1500", "imix", "imix_csum", "nat64",
-                             "nat64_4to6"])
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--config", default="parse64", choices=list(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--graph", action="store_true",
-                    help="parse configs: replay the launch cycle as a HIP graph (measured "
-                         "slower than direct launches on MI355X: kept for comparison)")
+    ap.add_argument("--only", action="store_true",
+                    help="time the --config only (no `shards` / `sizes` objects; for profiling)")
+    ap.add_argument("--sub-steps", type=int, default=300,
+                    help="timed launches of each `shards` / `sizes` config (at least --steps)")
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--e2e", action="store_true",
                     help="host-resident batches: pinned H2D + parse + D2H, pipelined (DESIGN.md §8)")
     ap.add_argument("--ingress", choices=["stage", "zero_copy"],
@@ -230,9 +450,20 @@ def main():
                     help="with --ingress: mbufs per cgpu_parse_mbufs call")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # Not started by torch.distributed.run: start one rank process per GPU
+        # (children of this process, which never touches the GPU).
+        from capsule_amd.shards import launch_ranks
+
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}; "
+              "using WORLD_SIZE", file=sys.stderr)
+    if args.stub:
+        return stub_worker(args)
+
     import torch
 
-    from capsule_amd import _native as N
     from capsule_amd import packets
     from capsule_amd.shards import ShardGroup
 
@@ -243,130 +474,32 @@ def main():
     g = ShardGroup()
     dev = torch.device("cuda", g.local_rank)
     torch.cuda.set_device(dev)
-    seed = g.shard_seed(0xC0FFEE + {"parse64": 2, "parse256": 2, "parse1500": 2, "imix": 3,
-                                    "imix_csum": 3, "nat64": 4, "nat64_4to6": 4}[args.config])
-    w = make_workload(args.config, seed)
-    n = len(w["off"])
     ctx = packets.Context(g.local_rank)
-    gw = nat64_4to6_setup(w, ctx, dev) if w["kind"] == "nat64_4to6" else None
 
-    # R resident copies so the rotation's footprint exceeds the Infinity Cache
-    batch_bytes = len(w["arena"]) + 6 * n
-    copies = max(2, -(-2 * INFINITY_CACHE // batch_bytes))
-    b0 = packets.PacketBatch.from_numpy(w["arena"], w["off"], w["len"], dev)
-    batches = [b0] + [packets.PacketBatch(b0.arena.clone(), b0.off.clone(), b0.len.clone())
-                      for _ in range(copies - 1)]
-    stream = torch.cuda.current_stream(dev)
-
-    if w["kind"] == "parse":
-        # checksum verify: CSUM_OK bits in meta, computed values not stored
-        outs = [packets.ParseBuffers(n, dev, csum=False) for _ in range(2)]
-
-        launchers = [packets.ParseLauncher(ctx, batches[k % copies], outs[k & 1], w["flags"],
-                                           stream) for k in range(2 * copies)]
-
-        def launch(k):
-            launchers[k % (2 * copies)]()
-    else:
-        direction = "4to6" if gw is not None else "6to4"
-        gw = gw or packets.Nat64Gateway(ctx, capacity_log2=17)
-        nat_out = [(torch.empty_like(b.arena), b.off, torch.empty(n, dtype=torch.int16, device=dev),
-                    torch.empty(n, dtype=torch.uint8, device=dev),
-                    torch.empty(n, dtype=torch.uint8, device=dev)) for b in batches[:2]]
-
-        launchers = [packets.Nat64Launcher(gw, batches[k % copies], nat_out[k & 1], stream,
-                                           direction) for k in range(2 * copies)]
-
-        def launch(k):
-            launchers[k % (2 * copies)]()
-
-    for k in range(args.warmup):
-        launch(k)
-    torch.cuda.synchronize(dev)
-
-    cycle = 2 * copies
-    if w["kind"] == "parse" and args.graph:
-        # Replay the launch cycle as a HIP graph (launch k still processes
-        # copy k mod R).  On MI355X the graph's node dispatch was measured at
-        # ~1 us per launch slower than direct back-to-back launches.
-        stream = torch.cuda.Stream(dev)
-        glaunch = [packets.ParseLauncher(ctx, batches[k % copies], outs[k & 1], w["flags"], stream)
-                   for k in range(cycle)]
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=stream):
-            for f in glaunch:
-                f()
-        torch.cuda.synchronize(dev)
-
-        whole = args.steps - args.steps % cycle  # timed launches covered by replays
-
-        def launch(k):  # noqa: F811 -- timed launch k (k >= warmup)
-            j = k - args.warmup
-            if j >= whole:
-                glaunch[j % cycle]()  # the remainder, launched directly
-            elif j % cycle == 0:
-                with torch.cuda.stream(stream):
-                    graph.replay()  # launches j .. j + cycle - 1
-
-    step = [0]
-    # HIP events on the launch stream bracket the K launches of the timed
-    # region: their span / K is the average device time per launch (kernel
-    # plus the back-to-back dispatch gap), without per-launch event overhead.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-
-    def one():
-        if step[0] == args.warmup:
-            ev0.record(stream)
-        launch(step[0])
-        step[0] += 1
-        if step[0] == args.warmup + args.steps:
-            ev1.record(stream)
-
-    step[0] = args.warmup
-    elapsed = g.timed(one, args.steps, sync=lambda: torch.cuda.synchronize(dev))
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
-    achieved = w["algo_bytes"] / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = ROOT / "profiles" / f"pmc_{args.config}.json"
-    if pmc.exists():  # PMC HBM bytes of this exact kernel source (scripts/summarize_prof.py)
-        sys.path.insert(0, str(ROOT / "scripts"))
-        from summarize_prof import source_hash
-
-        p = json.loads(pmc.read_text())
-        if p.get("src_hash") == source_hash(args.config) and "traffic_bytes" in p:
-            traffic = int(p["traffic_bytes"])
-
-    total_pkts = g.sum(n * args.steps)
-    value = total_pkts / elapsed / 1e6
-    frac_all = g.sum(achieved / HBM_PEAK_GBS) / g.world
-    result = {
-        "metric": "Mpps device-resident parse+cksum+hash @64/256/1500B; % HBM-read roofline",
-        "value": round(value, 2),
-        "unit": "Mpps",
-        "n_gpus": g.world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (seeded proptest-style reconciled frames, one shard per rank)",
-        "config": {"workload": w["desc"], "config": args.config, "packets_per_step": n,
-                   "global_batch": n * g.world, "resident_copies": copies,
-                   "launch": ("hip graph replays of %d launches" % cycle
-                              if w["kind"] == "parse" and args.graph else "direct"),
-                   "parallelism": f"{g.world} independent RX-queue shards (no collective)"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel_us": round(kern_ms * 1e3, 3),
-                     "algo_bytes_per_launch": w["algo_bytes"],
-                     "mean_frac_over_ranks": round(frac_all, 4)},
-    }
+    main_r = bench_config(args.config, g, ctx, dev, args.steps, args.warmup)
+    extra = {}
+    if not args.only:
+        sub = max(args.steps, args.sub_steps)
+        # BASELINE config 5: this rank's IMIX shard, all ranks at once
+        shard_r = (main_r if args.config == SHARD_CONFIG else
+                   bench_config(SHARD_CONFIG, g, ctx, dev, sub, args.warmup))
+        extra["shards"] = dict(summarize(shard_r, g), config=SHARD_CONFIG,
+                               roofline_basis="header bytes the reference touches + 6-B "
+                                              "descriptor (SURVEY.md §8d)")
+        if g.world == 1:  # the metric's other sizes and configs 3'/4 (N=1 only)
+            sizes = {}
+            for c in SIZES:
+                r = shard_r if c == SHARD_CONFIG else bench_config(c, g, ctx, dev, sub,
+                                                                     args.warmup)
+                sizes[c] = summarize(r, g)
+                if r is not shard_r:
+                    r["w"] = None
+            extra["sizes"] = sizes
+        shard_r["w"] = None if shard_r is not main_r else shard_r["w"]
+    cpu = None
     if g.world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
-    if g.rank == 0:
-        print(json.dumps(result), flush=True)
+        cpu = cpu_baseline(main_r["w"], args.cpu_seconds)
+    emit(args, g, main_r, extra, cpu)
     ctx.close()
     g.close()
 

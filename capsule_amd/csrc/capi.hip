@@ -34,6 +34,27 @@ int hip_fail(hipError_t e) {
   return fail(CGPU_EIO);
 }
 
+// Makes a context's device current for one entry point and gives the
+// calling thread its own current device back on return: a core thread may
+// drive contexts of several GPUs, and a NULL stream means "the current
+// device's", so every call that allocates, copies or launches runs inside
+// one of these.
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int dev) : dev_(dev) {
+    if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+    ok_ = prev_ == dev || hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev_ >= 0 && prev_ != dev_) (void)hipSetDevice(prev_);
+  }
+  bool ok() const { return ok_; }
+
+ private:
+  int dev_, prev_ = -1;
+  bool ok_ = false;
+};
+
 }  // namespace
 
 struct cgpu_ctx {
@@ -66,6 +87,10 @@ struct cgpu_portmap {
   uint32_t *defer = nullptr;
   uint32_t scratch_n = 0;
   uint32_t calls = 0;  // 6to4 calls: parity of the deferred-list counter
+  // the stream of the latest call: calls on one map are stream-ordered
+  // (the map is stateful), so draining it drains the map's work without
+  // stalling other contexts' streams on the same GPU
+  hipStream_t last = nullptr;
 };
 
 extern "C" {
@@ -118,7 +143,8 @@ int cgpu_ctx_create(int hip_device, cgpu_ctx **out) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || hip_device < 0 || hip_device >= count)
     return fail(CGPU_ENODEV);
-  if (hipSetDevice(hip_device) != hipSuccess) return fail(CGPU_ENODEV);
+  DeviceGuard dg(hip_device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
   cgpu_ctx *c = new (std::nothrow) cgpu_ctx();
   if (!c) return fail(CGPU_ENOMEM);
   c->device = hip_device;
@@ -132,7 +158,7 @@ int cgpu_ctx_create(int hip_device, cgpu_ctx **out) {
 
 void cgpu_ctx_destroy(cgpu_ctx *c) {
   if (!c) return;
-  (void)hipSetDevice(c->device);
+  DeviceGuard dg(c->device);
   if (c->h_arena) (void)hipHostFree(c->h_arena);
   if (c->d_arena) (void)hipFree(c->d_arena);
   if (c->h_desc) (void)hipHostFree(c->h_desc);
@@ -161,6 +187,8 @@ int cgpu_parse_batch(cgpu_ctx *ctx, const cgpu_batch *batch, uint32_t flags,
   if (batch->n == 0) return ok();
   if (!out->meta) return fail(CGPU_EINVAL);
   if ((flags & CGPU_F_FLOW_HASH) && !out->flow_hash) return fail(CGPU_EINVAL);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
   // no L3 (L4) type named: every IP version (UDP and TCP) accepted
   if ((flags & (CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6)) == 0) flags |= CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6;
   if ((flags & (CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP | CGPU_F_ACCEPT_ICMP)) == 0)
@@ -259,7 +287,8 @@ static int parse_and_return(cgpu_ctx *ctx, const uint8_t *arena, size_t arena_le
 template <class Get>
 static int parse_staged(cgpu_ctx *ctx, uint32_t n, Get get, uint32_t flags, uint32_t *meta,
                         uint32_t *csum, uint64_t *flow_hash, cgpu_hdr_record *fields) {
-  if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
   size_t total = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const uint8_t *p;
@@ -313,7 +342,8 @@ static int parse_zero_copy(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32
                            uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
                            cgpu_hdr_record *fields) {
   if (ctx->nreg == 0) return fail(CGPU_EINVAL);
-  if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
   constexpr uint32_t kChunk = 1u << 20;
   constexpr size_t kSlotMax = 2176;  // the mbuf buffer: 128 headroom + 2048 data room (align 64)
   const uint32_t m0 = n < kChunk ? n : kChunk;
@@ -375,7 +405,8 @@ int cgpu_parse_host(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *le
 
 int cgpu_host_register(cgpu_ctx *ctx, void *base, size_t bytes) {
   if (!ctx || !base || bytes == 0 || ctx->nreg >= cgpu::kMaxRegions) return fail(CGPU_EINVAL);
-  if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
   // Memory that is already page-locked (hipHostMalloc'd, or registered by
   // someone else) is only mapped; anything else is registered here.
   hipPointerAttribute_t attr;
@@ -405,7 +436,8 @@ int cgpu_host_unregister(cgpu_ctx *ctx, void *base) {
   if (!ctx || !base) return fail(CGPU_EINVAL);
   for (uint32_t r = 0; r < ctx->nreg; ++r) {
     if (ctx->reg[r].host_base != (uint64_t)(uintptr_t)base) continue;
-    if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
+    DeviceGuard dg(ctx->device);
+    if (!dg.ok()) return fail(CGPU_ENODEV);
     if (ctx->reg_owned[r] && hipHostUnregister(base) != hipSuccess) return fail(CGPU_EIO);
     for (uint32_t q = r + 1; q < ctx->nreg; ++q) {
       ctx->reg[q - 1] = ctx->reg[q];
@@ -439,7 +471,8 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
                         cgpu_portmap **out) {
   if (!ctx || !out || capacity_log2 < 4 || capacity_log2 > 29) return fail(CGPU_EINVAL);
   *out = nullptr;
-  if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
   const size_t cap = (size_t)1 << capacity_log2;
   const size_t bytes = 256 + 65536 * 8 + cap * sizeof(cgpu::PortSlot);
   void *mem = nullptr;
@@ -451,6 +484,7 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
   }
   pm->ctx = ctx;
   pm->mem = mem;
+  pm->last = ctx->stream;
   uint8_t *p = (uint8_t *)mem;
   pm->dev.state = (uint32_t *)p;
   pm->dev.rev = (uint64_t *)(p + 256);
@@ -468,17 +502,20 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
 
 void cgpu_portmap_destroy(cgpu_portmap *pm) {
   if (!pm) return;
-  (void)hipSetDevice(pm->ctx->device);
-  (void)hipDeviceSynchronize();
+  DeviceGuard dg(pm->ctx->device);
+  (void)hipStreamSynchronize(pm->last);
   if (pm->pkt_slot) (void)hipFree(pm->pkt_slot);
   (void)hipFree(pm->mem);
   delete pm;
 }
 
 static int read_state(cgpu_portmap *pm, uint32_t st[4]) {
-  if (hipSetDevice(pm->ctx->device) != hipSuccess) return CGPU_ENODEV;
-  if (hipDeviceSynchronize() != hipSuccess) return CGPU_EIO;
-  if (hipMemcpy(st, pm->dev.state, 16, hipMemcpyDeviceToHost) != hipSuccess) return CGPU_EIO;
+  DeviceGuard dg(pm->ctx->device);
+  if (!dg.ok()) return CGPU_ENODEV;
+  // behind the map's latest call, on its own stream
+  if (hipMemcpyAsync(st, pm->dev.state, 16, hipMemcpyDeviceToHost, pm->last) != hipSuccess ||
+      hipStreamSynchronize(pm->last) != hipSuccess)
+    return CGPU_EIO;
   return 0;
 }
 
@@ -507,6 +544,8 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   if (!out_arena || !out_off || !out_len || !disposition || !status) return fail(CGPU_EINVAL);
   if (out_arena_len > 0xffff0000ull) return fail(CGPU_EINVAL);
   if (in->n >= 0x7fffffffu) return fail(CGPU_EINVAL);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
   if (pm->scratch_n < in->n) {
     if (pm->pkt_slot) (void)hipFree(pm->pkt_slot);
     pm->pkt_slot = nullptr;
@@ -521,7 +560,8 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
     pm->pkt_slot = (uint32_t *)m;
     pm->lookback = (uint64_t *)((uint8_t *)m + o_sums);
     // status 0 = "not published" in every epoch
-    if (hipMemset(pm->lookback, 0, 8ull * nb) != hipSuccess) return fail(CGPU_EIO);
+    if (hipMemsetAsync(pm->lookback, 0, 8ull * nb, (hipStream_t)stream) != hipSuccess)
+      return fail(CGPU_EIO);
     pm->rec_h = (uint8_t *)m + o_rech;
     pm->rec_b = (uint8_t *)m + o_recb;
     pm->defer = (uint32_t *)((uint8_t *)m + o_defer);
@@ -551,6 +591,7 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
                      : cgpu::launch_nat64_4to6(a, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e);
   if (to4) ++pm->calls;
+  pm->last = (hipStream_t)stream;
   return ok();
 }
 
@@ -575,7 +616,8 @@ static int nat64_mbufs(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, void *const *m
   if (!ctx || !pm) return fail(CGPU_EINVAL);
   if (n == 0) return ok();
   if (!mbufs || !disposition || !status || ctx->nreg == 0) return fail(CGPU_EINVAL);
-  if (hipSetDevice(ctx->device) != hipSuccess) return fail(CGPU_ENODEV);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
   constexpr uint32_t kChunk = 1u << 20;
   constexpr size_t kSlotMax = 2176;  // >= round_up(2048 + 20, 64)
   const uint32_t m0 = n < kChunk ? n : kChunk;
@@ -671,6 +713,8 @@ int cgpu_group_by(cgpu_ctx *ctx, const void *key, uint32_t key_kind, uint32_t n,
     return ok();
   }
   if (!key || !idx) return fail(CGPU_EINVAL);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
   const uint32_t tiles = cgpu::group_by_tiles(n);
   const size_t need = (size_t)tiles * n_groups;
   if (ctx->gb_cap < need) {
@@ -701,6 +745,8 @@ int cgpu_set_ip(cgpu_ctx *ctx, uint8_t *arena, uint64_t arena_len, const uint32_
   if (!ctx || n > CGPU_MAX_BATCH || src_stride > 1u || dst_stride > 1u) return fail(CGPU_EINVAL);
   if (n == 0) return ok();
   if (!arena || !off || !len || !meta || arena_len > 0xffff0000ull) return fail(CGPU_EINVAL);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
   cgpu::SetIpArgs a;
   a.arena = arena;
   a.arena_len = (uint32_t)arena_len;

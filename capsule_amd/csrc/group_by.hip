@@ -32,7 +32,12 @@ __device__ __forceinline__ uint32_t arm_of(const GroupByArgs &a, uint32_t i) {
   if (a.kind == CGPU_KEY_META_CLASS) {
     const uint32_t m = static_cast<const uint32_t *>(a.key)[i];
     const uint32_t l3 = (m >> 16) & 3u, l4 = (m >> 18) & 3u;
-    k = (m & 0xffu) ? 4u : (((l3 == CGPU_L3_IPV6) ? 2u : 0u) | ((l4 == CGPU_L4_TCP) ? 1u : 0u));
+    // arms 0-3: the UDP/TCP classes; 4: failed parses and every other L4
+    // layer (ICMP), so no ICMP frame reaches a Udp or Tcp arm
+    const bool udp_tcp = l4 == CGPU_L4_UDP || l4 == CGPU_L4_TCP;
+    k = ((m & 0xffu) || !udp_tcp)
+            ? 4u
+            : (((l3 == CGPU_L3_IPV6) ? 2u : 0u) | ((l4 == CGPU_L4_TCP) ? 1u : 0u));
   } else {
     k = static_cast<const uint8_t *>(a.key)[i];
   }

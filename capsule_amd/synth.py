@@ -36,12 +36,23 @@ def _fold(s):
 
 
 def _be_word_sum(block):
-    """Sum of big-endian u16 words of each row (odd tail padded with 0)."""
+    """Sum of big-endian u16 words of each row (odd tail padded with 0).
+
+    Rows are summed in chunks of ~16 MiB so a 1 M x 1500-B block needs no
+    8-byte-per-byte temporary."""
     m, L = block.shape
-    if L % 2:
-        block = np.concatenate([block, np.zeros((m, 1), np.uint8)], axis=1)
-    w = block.reshape(m, -1, 2).astype(np.uint64)
-    return (w[:, :, 0] * np.uint64(256) + w[:, :, 1]).sum(axis=1)
+    out = np.zeros(m, np.uint64)
+    if m == 0 or L == 0:
+        return out
+    step = max(1, (16 << 20) // L)
+    for s in range(0, m, step):
+        b = block[s : s + step]
+        if L % 2:
+            b = np.concatenate([b, np.zeros((b.shape[0], 1), np.uint8)], axis=1)
+        else:
+            b = np.ascontiguousarray(b)
+        out[s : s + step] = b.view(">u2").sum(axis=1, dtype=np.uint64)
+    return out
 
 
 def _put16(a, col, v):
@@ -187,7 +198,9 @@ def place(groups, order, slot=64):
     """Lay out frames of several same-length groups in `order` into an arena.
 
     groups: list of [m_g, L_g] arrays; order: array of (group, row) pairs.
-    Returns (arena, off, len).
+    Returns (arena, off, len).  Every frame starts a run of whole `slot`-byte
+    blocks, so a group is scattered block-wise (one index per block, not
+    per byte), in chunks of rows.
     """
     lens = np.array([groups[g].shape[1] for g, _ in order], dtype=np.uint64)
     slots = (lens + np.uint64(slot - 1)) // np.uint64(slot) * np.uint64(slot)
@@ -197,15 +210,23 @@ def place(groups, order, slot=64):
     total = int(slots.sum()) if len(order) else 0
     assert total < (1 << 32), "arena must stay below 4 GiB (u32 offsets)"
     arena = np.zeros(max(total, slot), dtype=np.uint8)
+    blocks = arena[: arena.size // slot * slot].reshape(-1, slot)
     order = np.asarray(order)
     for g, arr in enumerate(groups):
         idx = np.nonzero(order[:, 0] == g)[0] if len(order) else np.zeros(0, np.int64)
         if not len(idx):
             continue
         L = arr.shape[1]
+        nb = max(1, -(-L // slot))
         rows = order[idx, 1]
-        dst = (off[idx][:, None] + np.arange(L, dtype=np.uint64)[None, :]).astype(np.int64)
-        arena[dst.reshape(-1)] = arr[rows].reshape(-1)
+        first = (off[idx] // np.uint64(slot)).astype(np.int64)
+        step = max(1, (32 << 20) // (nb * slot))
+        for c in range(0, len(idx), step):
+            r = rows[c : c + step]
+            pad = np.zeros((len(r), nb * slot), np.uint8)
+            pad[:, :L] = arr[r]
+            bi = first[c : c + step, None] + np.arange(nb)[None, :]
+            blocks[bi.reshape(-1)] = pad.reshape(-1, slot)
     return arena, off.astype(np.uint32), lens.astype(np.uint16)
 
 

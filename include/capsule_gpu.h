@@ -133,7 +133,7 @@ enum cgpu_pkt_status {
  * (buf_addr + data_off, data_len; mbuf.rs:196-205).  All pointers are
  * device pointers for the *_batch entry points.  arena_len must be <= 0xFFFF0000
  * and n <= CGPU_MAX_BATCH.                                                   */
-#define CGPU_MAX_BATCH (1u << 30)
+#define CGPU_MAX_BATCH ((1u << 30) - 1u) /* 4 * n bytes of off[] fit a 32-bit buffer range */
 typedef struct cgpu_batch {
   const uint8_t *arena;
   uint64_t arena_len;
@@ -346,7 +346,8 @@ int cgpu_nat64_mbufs(cgpu_ctx *ctx, cgpu_portmap *pm, uint32_t direction, void *
  * cgpu_disposition array.
  *   key_kind CGPU_KEY_U8:         key = const uint8_t[n] (e.g. disposition)
  *   key_kind CGPU_KEY_META_CLASS: key = const uint32_t[n] parse meta words;
- *     arm = 0 v4/UDP, 1 v4/TCP, 2 v6/UDP, 3 v6/TCP, 4 status != OK
+ *     arm = 0 v4/UDP, 1 v4/TCP, 2 v6/UDP, 3 v6/TCP, 4 everything else
+ *     (status != OK, or an L4 layer other than UDP/TCP, i.e. ICMP)
  * idx[n]: packet indices grouped by arm; group_off[n_groups + 1]: arm k owns
  * idx[group_off[k] .. group_off[k+1]).  n_groups in 1..64, n <= 2^28.  All
  * device pointers; asynchronous on `stream`.  Uses per-context scratch: one

@@ -731,6 +731,7 @@ void or_nat64_6to4(or_portmap *pm, const uint8_t *arena, const uint32_t *off, co
 static uint32_t meta_class(uint32_t m) {
   if ((m & 0xffu) != CGPU_PKT_OK) return 4;
   const uint32_t l3 = (m >> 16) & 3u, l4 = (m >> 18) & 3u;
+  if (l4 != CGPU_L4_UDP && l4 != CGPU_L4_TCP) return 4; /* ICMP: neither Udp nor Tcp */
   if (l3 == CGPU_L3_IPV4) return l4 == CGPU_L4_TCP ? 1 : 0;
   return l4 == CGPU_L4_TCP ? 3 : 2;
 }

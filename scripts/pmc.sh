@@ -9,7 +9,7 @@ n=0
 for ctrs in "$@"; do
   n=$((n+1))
   OUT=$REPO/gpurun_out/pmc_${CFG}_$n
-  timeout -k 10 300 rocprofv3 --pmc $ctrs -d $OUT -o pmc --output-format csv -- python3 $REPO/bench.py --config $CFG --steps 30 --warmup 5 --no-cpu > $OUT.log 2>&1 || { echo "pmc pass $n rc=$?"; tail -5 $OUT.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $ctrs -d $OUT -o pmc --output-format csv -- python3 $REPO/bench.py --config $CFG --steps 30 --warmup 5 --no-cpu --only > $OUT.log 2>&1 || { echo "pmc pass $n rc=$?"; tail -5 $OUT.log; exit 1; }
   python3 - $OUT <<'PY'
 import csv, sys, glob, collections
 f = glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)[0]

@@ -13,7 +13,7 @@ cd /tmp
 run() {  # name, limit, rocprof args...
   local name=$1 lim=$2; shift 2
   timeout -k 10 "$lim" rocprofv3 "$@" -d "$OUT/$name" -o "$name" --output-format csv \
-      -- python3 "$REPO/bench.py" --no-cpu $ARGS > "$OUT/$name.log" 2>&1
+      -- python3 "$REPO/bench.py" --no-cpu --only $ARGS > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"; tail -2 "$OUT/$name.log"
   if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi

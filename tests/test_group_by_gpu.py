@@ -65,6 +65,30 @@ def test_group_by_parse_class(ctx):
         _check(ctx, meta, groups, N.KEY_META_CLASS)
 
 
+def test_group_by_parse_class_icmp(ctx):
+    """ICMPv4/ICMPv6 frames parsed with CGPU_F_ACCEPT_ICMP land in the
+    catch-all arm, never in a Udp or Tcp arm."""
+    from capsule_amd import packets
+
+    rng = np.random.default_rng(11)
+    kinds = [synth.V4_UDP, synth.V4_TCP, synth.V6_UDP, synth.V6_TCP, synth.V4_ICMP,
+             synth.V6_ICMP]
+    frames = [bytes(synth.build_frames(rng, 1, kinds[k], 120)[0])
+              for k in rng.integers(0, len(kinds), 6000)]
+    a, o, l = synth.pack_frames(frames)
+    r = packets.parse(ctx, packets.PacketBatch.from_numpy(a, o, l, DEV),
+                      N.F_ACCEPT_ALL | N.F_ACCEPT_ICMP | N.F_CSUM_L4)
+    torch.cuda.synchronize()
+    meta = r.meta.cpu().numpy().view(np.uint32)
+    l4 = (meta >> 18) & 3
+    assert ((meta & 0xFF) == 0).all() and (l4 == N.L4_ICMP).sum() > 1000
+    off = _check(ctx, meta, 5, N.KEY_META_CLASS)
+    icmp = set(np.nonzero(l4 == N.L4_ICMP)[0].tolist())
+    idx, _ = oracle_lib.group_by(meta, 5, N.KEY_META_CLASS)
+    assert icmp <= set(idx[off[4]:off[5]].tolist())
+    assert not icmp & set(idx[:off[4]].tolist())
+
+
 def test_group_by_nat64_dispositions(ctx):
     """Send::run (batch/send.rs:95-118) on a nat64 burst: the Act arm is the
     tx list, arm sizes are the emitted / dropped / aborted counters."""

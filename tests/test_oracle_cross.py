@@ -151,3 +151,16 @@ def test_oracle_group_by_is_stable_partition():
         ref = np.argsort(arm, kind="stable")
         assert (idx == ref).all()
         assert (off == np.concatenate([[0], np.cumsum(np.bincount(arm, minlength=g))])).all()
+
+
+def test_oracle_group_by_meta_class_arms():
+    """CGPU_KEY_META_CLASS: v4/UDP, v4/TCP, v6/UDP, v6/TCP, then everything
+    else -- failed parses and ICMP (which is neither Udp nor Tcp)."""
+    def meta(status, l3, l4):
+        return status | (l3 << 16) | (l4 << 18)
+
+    m = np.array([meta(0, 1, 1), meta(0, 1, 2), meta(0, 2, 1), meta(0, 2, 2),
+                  meta(0, 1, 3), meta(0, 2, 3), meta(8, 1, 0), meta(0, 1, 1)], np.uint32)
+    idx, off = oracle_lib.group_by(m, 5, N.KEY_META_CLASS)
+    assert off.tolist() == [0, 2, 3, 4, 5, 8]
+    assert idx.tolist() == [0, 7, 1, 2, 3, 4, 5, 6]

@@ -57,3 +57,75 @@ def test_two_rank_gloo_shards(tmp_path):
     assert a["ok"] and b["ok"]
     assert a["total"] == b["total"] == 4000                 # aggregate = sum of shards
     assert abs(a["t"] - b["t"]) < 1e-9 and a["t"] >= 0.06   # max over ranks (rank 1 slower)
+
+
+def _bench_line(out):
+    import json
+
+    lines = [x for x in out.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out[-2000:]  # rank 0 prints exactly one JSON line
+    return json.loads(lines[0])
+
+
+def _stub_env():
+    return dict(os.environ, OMP_NUM_THREADS="1")
+
+
+def test_bench_launcher_spawns_n_ranks():
+    """`bench.py --gpus 2` without torch.distributed.run starts two rank
+    processes itself (GPU-free worker stub here) and reports both."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--stub", "--steps", "3",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=300,
+                       env=_stub_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _bench_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * d["config"]["packets_per_step"]
+    assert [x["rank"] for x in d["roofline"]["per_rank"]] == [0, 1]
+    sh = d["shards"]
+    assert [x["rank"] for x in sh["per_rank"]] == [0, 1] and sh["config"] == "imix"
+    # rank 1's stub launches are twice as slow: max over ranks sets the time
+    assert sh["per_rank"][1]["kernel_us"] == 2 * sh["per_rank"][0]["kernel_us"]
+    assert "sizes" not in d and "cpu_baseline" not in d  # N=1-only objects
+    assert d["scaling"] == "weak" and "no collective" in d["config"]["parallelism"]
+
+
+def test_bench_under_torchrun_stub():
+    """The driver's own launch (torch.distributed.run, WORLD_SIZE set): no
+    second launcher, the ranks join one gloo group."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr=127.0.0.1",
+                        f"--master-port={port}", "bench.py", "--gpus", "2", "--stub",
+                        "--steps", "3", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, env=_stub_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _bench_line(r.stdout)
+    assert d["n_gpus"] == 2 and len(d["shards"]["per_rank"]) == 2
+
+
+def test_bench_single_gpu_line_shape():
+    """N=1: the metric line plus `shards` (config 5 at N=1) and `sizes`
+    (the metric's other sizes and configs 3/3'/4)."""
+    r = subprocess.run([sys.executable, "bench.py", "--stub", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, env=_stub_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _bench_line(r.stdout)
+    assert d["n_gpus"] == 1 and d["steps"] == 2
+    for k in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "dtype",
+              "config", "roofline"):
+        assert k in d
+    assert set(d["sizes"]) == {"parse256", "parse1500", "imix", "imix_csum", "nat64"}
+    assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(d["roofline"])
+    assert "unpinned" in d["parity"]["flow_hash"]
+
+
+def test_shard_group_refuses_device_backend():
+    from capsule_amd.shards import ShardGroup
+    import pytest
+
+    with pytest.raises(ValueError):
+        ShardGroup(backend="nccl")
