@@ -65,8 +65,10 @@ struct cgpu_ctx {
   size_t arena_cap = 0;
   uint8_t *h_desc = nullptr, *d_desc = nullptr;  // off[n] | len[n] | outputs
   size_t desc_cap = 0;
-  uint8_t *d_out = nullptr;       // nat64 over mbufs: the rewritten frames
-  size_t out_cap = 0;
+  // zero-copy ingress: the device arena the gather lays bursts out in, and
+  // (nat64 over mbufs) the rewritten frames; both grow on demand
+  uint8_t *d_zc = nullptr, *d_out = nullptr;
+  size_t zc_cap = 0, out_cap = 0;
   uint32_t *gb_counts = nullptr;  // cgpu_group_by scratch
   size_t gb_cap = 0;              // entries
   // host regions registered for zero-copy ingress
@@ -91,6 +93,7 @@ struct cgpu_portmap {
   // (the map is stateful), so draining it drains the map's work without
   // stalling other contexts' streams on the same GPU
   hipStream_t last = nullptr;
+  uint32_t room = 2048u;  // Nat64Args::room of the next call (65535 inside cgpu_nat64_mbufs)
 };
 
 extern "C" {
@@ -165,6 +168,7 @@ void cgpu_ctx_destroy(cgpu_ctx *c) {
   if (c->d_desc) (void)hipFree(c->d_desc);
   if (c->gb_counts) (void)hipFree(c->gb_counts);
   if (c->d_out) (void)hipFree(c->d_out);
+  if (c->d_zc) (void)hipFree(c->d_zc);
   for (uint32_t r = 0; r < c->nreg; ++r)
     if (c->reg_owned[r]) (void)hipHostUnregister((void *)(uintptr_t)c->reg[r].host_base);
   (void)hipStreamDestroy(c->stream);
@@ -336,53 +340,108 @@ static inline void mbuf_fields(const void *m, const uint8_t *&data, uint16_t &le
   data = buf_addr + data_off;
 }
 
-// Zero-copy: the device gathers the burst from registered host memory,
-// in chunks of at most 2^20 mbufs (a chunk's arena stays below 4 GiB).
+static int grow_dev(uint8_t **d, size_t *cap, size_t need) {
+  if (need <= *cap) return 0;
+  if (*d) (void)hipFree(*d);
+  *d = nullptr;
+  *cap = 0;
+  if (hipMalloc((void **)d, need) != hipSuccess) return CGPU_ENOMEM;
+  *cap = need;
+  return 0;
+}
+
+namespace {
+
+// Zero-copy gathers work in chunks of at most 2^20 mbufs whose arena stays
+// below 4 GiB (u32 offsets); a chunk of jumbo frames that would not fit is
+// cut shorter.
+constexpr uint32_t kZcChunk = 1u << 20;
+constexpr size_t kZcSlot = 2176;                  // an mbuf buffer: 128 headroom + 2048 room
+constexpr uint64_t kZcArenaMax = 0xffff0000ull;   // cgpu_batch::arena_len limit
+
+struct ZcCounters {  // device counters of one gather (16 bytes)
+  unsigned long long cursor;
+  uint32_t bad, pad;
+};
+
+// One zero-copy gather of mbufs[at, at + m) (the pointer array already at
+// `ptrs` on the device).  arena = nullptr: validate the pointers only.
+hipError_t gather_chunk(cgpu_ctx *ctx, const uint64_t *ptrs, uint32_t m, uint8_t *arena,
+                        size_t arena_cap, uint32_t *off, uint16_t *len, ZcCounters *cnt,
+                        uint32_t slot_extra, uint8_t *egress_base, uint32_t stride,
+                        hipStream_t s) {
+  if (hipMemsetAsync(cnt, 0, sizeof(ZcCounters), s) != hipSuccess) return hipErrorUnknown;
+  cgpu::GatherArgs g;
+  g.mbufs = ptrs;
+  g.n = m;
+  g.nreg = ctx->nreg;
+  for (uint32_t r = 0; r < cgpu::kMaxRegions; ++r) g.reg[r] = ctx->reg[r];
+  g.arena = arena;
+  g.arena_cap = arena_cap;
+  g.off = off;
+  g.len = len;
+  g.cursor = &cnt->cursor;
+  g.bad = &cnt->bad;
+  g.slot_extra = slot_extra;
+  g.mb_dev = g.fr_dev = nullptr;
+  g.pkt_len = g.tailroom = nullptr;
+  if (egress_base) {  // per-mbuf egress records: mb | fr | pkt_len | tailroom, `stride` each
+    g.mb_dev = (uint64_t *)egress_base;
+    g.fr_dev = g.mb_dev + stride;
+    g.pkt_len = (uint32_t *)(g.fr_dev + stride);
+    g.tailroom = g.pkt_len + stride;
+  }
+  return cgpu::launch_mbuf_gather(g, s);
+}
+
+}  // namespace
+
+// Zero-copy: the device gathers the burst from registered host memory.  The
+// parse runs right behind the gather; if the chunk's frames did not fit the
+// arena (a jumbo mempool), the arena grows and the chunk is done again.
 static int parse_zero_copy(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32_t flags,
                            uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
                            cgpu_hdr_record *fields) {
   if (ctx->nreg == 0) return fail(CGPU_EINVAL);
   DeviceGuard dg(ctx->device);
   if (!dg.ok()) return fail(CGPU_ENODEV);
-  constexpr uint32_t kChunk = 1u << 20;
-  constexpr size_t kSlotMax = 2176;  // the mbuf buffer: 128 headroom + 2048 data room (align 64)
-  const uint32_t m0 = n < kChunk ? n : kChunk;
-  if (int e = grow(&ctx->h_arena, &ctx->d_arena, &ctx->arena_cap, (size_t)m0 * kSlotMax + 64))
-    return fail(e);
+  const uint32_t m0 = n < kZcChunk ? n : kZcChunk;
+  if (int e = grow_dev(&ctx->d_zc, &ctx->zc_cap, (size_t)m0 * kZcSlot + 64)) return fail(e);
   const size_t ptrs = 0, counters = align_up(8ull * m0, 256);
   const HostLayout lay(m0, fields != nullptr, counters + 256);
   if (int e = grow(&ctx->h_desc, &ctx->d_desc, &ctx->desc_cap, lay.end)) return fail(e);
   hipStream_t s = ctx->stream;
+  uint8_t *D = ctx->d_desc, *H = ctx->h_desc;
+  ZcCounters *dcnt = (ZcCounters *)(D + counters), *hcnt = (ZcCounters *)(H + counters);
   uint32_t bad_total = 0;
-  for (uint32_t at = 0; at < n; at += m0) {
-    const uint32_t m = n - at < m0 ? n - at : m0;
-    memcpy(ctx->h_desc + ptrs, mbufs + at, 8ull * m);
-    if (hipMemcpyAsync(ctx->d_desc + ptrs, ctx->h_desc + ptrs, 8ull * m, hipMemcpyHostToDevice, s) !=
-            hipSuccess ||
-        hipMemsetAsync(ctx->d_desc + counters, 0, 8, s) != hipSuccess)
-      return fail(CGPU_EIO);
-    cgpu::GatherArgs g;
-    g.mbufs = (const uint64_t *)(ctx->d_desc + ptrs);
-    g.n = m;
-    g.nreg = ctx->nreg;
-    for (uint32_t r = 0; r < cgpu::kMaxRegions; ++r) g.reg[r] = ctx->reg[r];
-    g.arena = ctx->d_arena;
-    g.off = (uint32_t *)(ctx->d_desc + lay.off);
-    g.len = (uint16_t *)(ctx->d_desc + lay.len);
-    g.cursor = (uint32_t *)(ctx->d_desc + counters);
-    g.bad = g.cursor + 1;
-    g.slot_extra = 0;
-    g.mb_dev = g.fr_dev = nullptr;
-    g.pkt_len = g.tailroom = nullptr;
-    if (cgpu::launch_mbuf_gather(g, s) != hipSuccess) return fail(CGPU_EIO);
-    if (int e = parse_and_return(ctx, ctx->d_arena, (size_t)m * kSlotMax + 64, m, lay, flags, meta,
-                                 csum, flow_hash, fields, at))
-      return e;
-    uint32_t *hcnt = (uint32_t *)(ctx->h_desc + counters);
-    if (hipMemcpyAsync(hcnt, ctx->d_desc + counters, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-      return fail(CGPU_EIO);
-    bad_total += hcnt[1];
+  for (uint32_t at = 0; at < n;) {
+    uint32_t m = n - at < m0 ? n - at : m0;
+    for (;;) {
+      memcpy(H + ptrs, mbufs + at, 8ull * m);
+      if (hipMemcpyAsync(D + ptrs, H + ptrs, 8ull * m, hipMemcpyHostToDevice, s) != hipSuccess)
+        return fail(CGPU_EIO);
+      const size_t cap = ctx->zc_cap < kZcArenaMax ? ctx->zc_cap : kZcArenaMax;
+      if (gather_chunk(ctx, (const uint64_t *)(D + ptrs), m, ctx->d_zc, cap,
+                       (uint32_t *)(D + lay.off), (uint16_t *)(D + lay.len), dcnt, 0, nullptr,
+                       0, s) != hipSuccess)
+        return fail(CGPU_EIO);
+      if (int e = parse_and_return(ctx, ctx->d_zc, cap, m, lay, flags, meta, csum, flow_hash,
+                                   fields, at))
+        return e;
+      if (hipMemcpyAsync(hcnt, dcnt, sizeof(ZcCounters), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+        return fail(CGPU_EIO);
+      const uint64_t need = hcnt->cursor + 64;
+      if (need <= cap) break;
+      if (need > kZcArenaMax) {  // fewer mbufs in this chunk
+        m = (uint32_t)((uint64_t)m * (kZcArenaMax / 2) / need);
+        if (m == 0) m = 1;
+        continue;
+      }
+      if (int e = grow_dev(&ctx->d_zc, &ctx->zc_cap, need)) return fail(e);
+    }
+    bad_total += hcnt->bad;
+    at += m;
   }
   return bad_total ? fail(CGPU_EINVAL) : ok();
 }
@@ -586,6 +645,7 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   a.rec_b = (uint2 *)pm->rec_b;
   a.defer = pm->defer;
   a.par = pm->calls & 1u;
+  a.room = pm->room;
   a.pm = pm->dev;
   hipError_t e = to4 ? cgpu::launch_nat64_6to4(a, (hipStream_t)stream)
                      : cgpu::launch_nat64_4to6(a, (hipStream_t)stream);
@@ -610,7 +670,10 @@ int cgpu_nat64_4to6(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8
 }
 
 // nat64 over an rte_mbuf burst: zero-copy gather, the device rewrite, the
-// ACT frames scattered back into their mbufs (cgpu_nat64_mbufs).
+// ACT frames scattered back into their mbufs (cgpu_nat64_mbufs).  The call
+// is all or nothing: every mbuf pointer and frame is validated before the
+// first frame is rewritten or the port map changes (a burst of more than one
+// chunk is validated chunk by chunk first).
 static int nat64_mbufs(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, void *const *mbufs, uint32_t n,
                        uint8_t *disposition, uint8_t *status) {
   if (!ctx || !pm) return fail(CGPU_EINVAL);
@@ -618,82 +681,95 @@ static int nat64_mbufs(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, void *const *m
   if (!mbufs || !disposition || !status || ctx->nreg == 0) return fail(CGPU_EINVAL);
   DeviceGuard dg(ctx->device);
   if (!dg.ok()) return fail(CGPU_ENODEV);
-  constexpr uint32_t kChunk = 1u << 20;
-  constexpr size_t kSlotMax = 2176;  // >= round_up(2048 + 20, 64)
-  const uint32_t m0 = n < kChunk ? n : kChunk;
-  const size_t arena_bytes = (size_t)m0 * kSlotMax + 64;
-  if (int e = grow(&ctx->h_arena, &ctx->d_arena, &ctx->arena_cap, arena_bytes)) return fail(e);
-  if (ctx->out_cap < arena_bytes) {
-    if (ctx->d_out) (void)hipFree(ctx->d_out);
-    ctx->d_out = nullptr;
-    ctx->out_cap = 0;
-    if (hipMalloc(&ctx->d_out, arena_bytes) != hipSuccess) return fail(CGPU_ENOMEM);
-    ctx->out_cap = arena_bytes;
-  }
-  // descriptor area: ptrs | off | len | out_len | disp | status | mb | fr | pkt_len | room | counters
+  const uint32_t m0 = n < kZcChunk ? n : kZcChunk;
+  const size_t want = (size_t)m0 * kZcSlot + 64;  // >= round_up(2048 + 20, 64) per frame
+  if (int e = grow_dev(&ctx->d_zc, &ctx->zc_cap, want)) return fail(e);
+  if (int e = grow_dev(&ctx->d_out, &ctx->out_cap, want)) return fail(e);
+  // descriptor area: ptrs | off | len | out_len | disp | status | egress records | counters
   const size_t o_ptr = 0, o_off = align_up(8ull * m0, 256), o_len = o_off + align_up(4ull * m0, 256);
   const size_t o_olen = o_len + align_up(2ull * m0, 256), o_disp = o_olen + align_up(2ull * m0, 256);
-  const size_t o_st = o_disp + align_up(m0, 256), o_mb = o_st + align_up(m0, 256);
-  const size_t o_fr = o_mb + align_up(8ull * m0, 256), o_pl = o_fr + align_up(8ull * m0, 256);
-  const size_t o_tr = o_pl + align_up(4ull * m0, 256), o_cnt = o_tr + align_up(4ull * m0, 256);
+  const size_t o_st = o_disp + align_up(m0, 256), o_eg = o_st + align_up(m0, 256);
+  const size_t o_cnt = o_eg + align_up(24ull * m0, 256);
   if (int e = grow(&ctx->h_desc, &ctx->d_desc, &ctx->desc_cap, o_cnt + 256)) return fail(e);
   uint8_t *D = ctx->d_desc, *H = ctx->h_desc;
+  ZcCounters *dcnt = (ZcCounters *)(D + o_cnt), *hcnt = (ZcCounters *)(H + o_cnt);
   hipStream_t s = ctx->stream;
-  uint32_t bad_total = 0;
-  for (uint32_t at = 0; at < n; at += m0) {
-    const uint32_t m = n - at < m0 ? n - at : m0;
+  const uint32_t slot_extra = to4 ? 0u : 20u;  // 4to6 frames grow by 20 B in their slot
+  auto upload = [&](uint32_t at, uint32_t m) {
     memcpy(H + o_ptr, mbufs + at, 8ull * m);
-    if (hipMemcpyAsync(D + o_ptr, H + o_ptr, 8ull * m, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemsetAsync(D + o_cnt, 0, 8, s) != hipSuccess)
-      return fail(CGPU_EIO);
-    cgpu::GatherArgs g;
-    g.mbufs = (const uint64_t *)(D + o_ptr);
-    g.n = m;
-    g.nreg = ctx->nreg;
-    for (uint32_t r = 0; r < cgpu::kMaxRegions; ++r) g.reg[r] = ctx->reg[r];
-    g.arena = ctx->d_arena;
-    g.off = (uint32_t *)(D + o_off);
-    g.len = (uint16_t *)(D + o_len);
-    g.cursor = (uint32_t *)(D + o_cnt);
-    g.bad = g.cursor + 1;
-    g.slot_extra = to4 ? 0u : 20u;  // 4to6 frames grow by 20 B in their slot
-    g.mb_dev = (uint64_t *)(D + o_mb);
-    g.fr_dev = (uint64_t *)(D + o_fr);
-    g.pkt_len = (uint32_t *)(D + o_pl);
-    g.tailroom = (uint32_t *)(D + o_tr);
-    if (cgpu::launch_mbuf_gather(g, s) != hipSuccess) return fail(CGPU_EIO);
+    return hipMemcpyAsync(D + o_ptr, H + o_ptr, 8ull * m, hipMemcpyHostToDevice, s) == hipSuccess;
+  };
+  if (n > m0) {  // validate every chunk before anything is written
+    uint32_t bad = 0;
+    for (uint32_t at = 0; at < n; at += m0) {
+      const uint32_t m = n - at < m0 ? n - at : m0;
+      if (!upload(at, m) ||
+          gather_chunk(ctx, (const uint64_t *)(D + o_ptr), m, nullptr, 0, nullptr, nullptr, dcnt,
+                       0, nullptr, 0, s) != hipSuccess ||
+          hipMemcpyAsync(hcnt, dcnt, sizeof(ZcCounters), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+        return fail(CGPU_EIO);
+      bad += hcnt->bad;
+    }
+    if (bad) return fail(CGPU_EINVAL);
+  }
+  for (uint32_t at = 0; at < n;) {
+    uint32_t m = n - at < m0 ? n - at : m0;
+    size_t cap;
+    for (;;) {
+      cap = ctx->zc_cap < kZcArenaMax ? ctx->zc_cap : kZcArenaMax;
+      if (!upload(at, m) ||
+          gather_chunk(ctx, (const uint64_t *)(D + o_ptr), m, ctx->d_zc, cap,
+                       (uint32_t *)(D + o_off), (uint16_t *)(D + o_len), dcnt, slot_extra,
+                       D + o_eg, m0, s) != hipSuccess ||
+          hipMemcpyAsync(hcnt, dcnt, sizeof(ZcCounters), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+        return fail(CGPU_EIO);
+      if (hcnt->bad) return fail(CGPU_EINVAL);  // before any rewrite of this burst
+      const uint64_t need = hcnt->cursor + 64;
+      if (need <= cap) break;
+      if (need > kZcArenaMax) {
+        m = (uint32_t)((uint64_t)m * (kZcArenaMax / 2) / need);
+        if (m == 0) m = 1;
+        continue;
+      }
+      if (int e = grow_dev(&ctx->d_zc, &ctx->zc_cap, need)) return fail(e);
+      if (int e = grow_dev(&ctx->d_out, &ctx->out_cap, need)) return fail(e);
+    }
     cgpu_batch in;
-    in.arena = ctx->d_arena;
-    in.arena_len = arena_bytes;
-    in.off = g.off;
-    in.len = g.len;
+    in.arena = ctx->d_zc;
+    in.arena_len = cap;
+    in.off = (const uint32_t *)(D + o_off);
+    in.len = (const uint16_t *)(D + o_len);
     in.n = m;
-    if (int e = nat64_call(to4, ctx, pm, &in, ctx->d_out, arena_bytes, g.off, (uint16_t *)(D + o_olen),
-                           D + o_disp, D + o_st, s))
-      return e;
+    pm->room = 65535u;  // the scatter applies each mbuf's real tailroom
+    const int e = nat64_call(to4, ctx, pm, &in, ctx->d_out, cap, in.off,
+                             (uint16_t *)(D + o_olen), D + o_disp, D + o_st, s);
+    pm->room = 2048u;
+    if (e) return e;
+    const uint64_t *mb = (const uint64_t *)(D + o_eg);
     cgpu::ScatterArgs sc;
     sc.out_arena = ctx->d_out;
-    sc.out_off = g.off;
+    sc.out_off = in.off;
     sc.out_len = (const uint16_t *)(D + o_olen);
     sc.disposition = D + o_disp;
     sc.status = D + o_st;
-    sc.mb_dev = g.mb_dev;
-    sc.fr_dev = g.fr_dev;
-    sc.pkt_len = g.pkt_len;
-    sc.tailroom = g.tailroom;
-    sc.in_len = g.len;
+    sc.mb_dev = mb;
+    sc.fr_dev = mb + m0;
+    sc.pkt_len = (const uint32_t *)(mb + 2 * (size_t)m0);
+    sc.tailroom = sc.pkt_len + m0;
+    sc.in_len = in.len;
     sc.n = m;
     sc.delta = to4 ? -20 : 20;
     if (cgpu::launch_mbuf_scatter(sc, s) != hipSuccess) return fail(CGPU_EIO);
-    if (hipMemcpyAsync(H + o_disp, D + o_disp, o_mb - o_disp, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(H + o_cnt, D + o_cnt, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemcpyAsync(H + o_disp, D + o_disp, o_eg - o_disp, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
       return fail(CGPU_EIO);
     memcpy(disposition + at, H + o_disp, m);
     memcpy(status + at, H + o_st, m);
-    bad_total += ((uint32_t *)(H + o_cnt))[1];
+    at += m;
   }
-  return bad_total ? fail(CGPU_EINVAL) : ok();
+  return ok();
 }
 
 int cgpu_nat64_mbufs(cgpu_ctx *ctx, cgpu_portmap *pm, uint32_t direction, void *const *mbufs,

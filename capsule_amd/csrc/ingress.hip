@@ -13,8 +13,9 @@
 // allocates its slots with one atomic, and then 16-lane groups copy four
 // frames at a time, 16 B per lane, all of a wave's first-256-B loads in
 // flight before any store.  Every host address is translated through the
-// registered regions and range-checked first: a pointer outside them is
-// counted (the call fails) and never dereferenced.
+// registered regions and range-checked first: a pointer outside them, or a
+// frame that runs past its own buffer, is counted (the call fails) and never
+// dereferenced.  No slot is written past the arena's capacity.
 #include "capsule_gpu.h"
 #include "device_common.hpp"
 #include "kernels.hpp"
@@ -70,8 +71,9 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
     const uint64_t dmm = __shfl(dm, (int)m);
     const bool okm = __shfl((int)mok, (int)m) != 0;
     H[r] = u32x4{0u, 0u, 0u, 0u};
-    // bytes 48..63 (buf_len @54) only for the egress path
-    if (okm && (q < 3u || g.tailroom)) H[r] = *reinterpret_cast<const u32x4 *>(dmm + 16u * q);
+    // the whole 64-B segment: buf_addr @0, data_off @16, pkt_len @36,
+    // data_len @40, buf_len @54
+    if (okm) H[r] = *reinterpret_cast<const u32x4 *>(dmm + 16u * q);
   }
   const uint32_t r_own = lane >> 4, src_lane = 4u * (lane & 15u);
   uint32_t ba_lo = 0, ba_hi = 0, doff = 0, dlen = 0, plen = 0, blen = 0;
@@ -95,8 +97,11 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
   uint32_t L = 0;
   bool ok = false;
   if (mok) {
+    // the frame lies in its own buffer (data_off + data_len <= buf_len, the
+    // invariant of every mbuf Mbuf::extend / shrink maintain) and in a
+    // registered region
     const uint64_t buf_addr = ((uint64_t)ba_hi << 32) | ba_lo;
-    ok = dlen == 0u || translate(g, buf_addr + doff, dlen, src);
+    ok = doff + dlen <= blen && (dlen == 0u || translate(g, buf_addr + doff, dlen, src));
     L = ok ? dlen : 0u;
     if (!ok) atomicAdd(g.bad, 1u);
   }
@@ -106,6 +111,7 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
     g.pkt_len[i] = plen;
     g.tailroom[i] = (blen - doff - dlen) & 0xffffu;  // u16 arithmetic, as Mbuf::tailroom
   }
+  if (!g.arena) return;  // validate only (wave-uniform)
   // --- slots: one atomic per wave, prefix within the wave ---------------------
   const uint32_t slot = (L + g.slot_extra + 63u) & ~63u;
   uint32_t incl = slot;
@@ -115,10 +121,15 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
     if (lane >= (uint32_t)d) incl += y;
   }
   const uint32_t total = __shfl(incl, 63);
-  uint32_t base = 0;
-  if (lane == 0u && total) base = atomicAdd(g.cursor, total);
+  uint64_t base = 0;
+  if (lane == 0u && total) base = atomicAdd(g.cursor, (unsigned long long)total);
   base = __shfl(base, 0);
-  const uint32_t o = base + incl - slot;
+  // A slot past the arena is not written (the frame reads as empty); the
+  // cursor still counts it, and the host redoes the chunk with an arena of
+  // the size the cursor reports (frames of a jumbo mempool).
+  const uint64_t o64 = base + incl - slot;
+  if (o64 + slot > g.arena_cap) L = 0u;
+  const uint32_t o = (uint32_t)o64;
   if (valid) {
     g.off[i] = o;
     g.len[i] = (uint16_t)L;

@@ -71,6 +71,9 @@ struct Nat64Args {
   uint2 *rec_b;          // scratch [n]: header dword 4, VLAN depth
   uint32_t *defer;       // scratch [n]: indices of the deferred 6to4 frames
   uint32_t par;          // call parity: selects the deferred-list counter state[4 + par]
+  uint32_t room;         // data room of Mbuf::extend's tailroom model (mbuf.rs:225-233):
+                         // 2048 for device batches; 65535 on the mbuf path, whose
+                         // scatter checks each mbuf's real tailroom instead
   PortMapDev pm;
 };
 
@@ -89,11 +92,14 @@ struct GatherArgs {
   uint32_t n;
   uint32_t nreg;
   HostRegion reg[kMaxRegions];
-  uint8_t *arena;         // device arena, 64-B slots
+  uint8_t *arena;         // device arena, 64-B slots; nullptr: validate only (no copy)
+  uint64_t arena_cap;     // bytes of `arena`: no slot is written past it
   uint32_t *off;          // [n]
   uint16_t *len;          // [n]
-  uint32_t *cursor;       // slot allocation cursor (zero before the launch)
-  uint32_t *bad;          // mbufs / frames outside every registered region
+  unsigned long long *cursor;  // slot allocation cursor (zero before the launch); after
+                               // it, the bytes the chunk needs (> arena_cap: redo bigger)
+  uint32_t *bad;          // mbufs / frames outside every registered region, or frames
+                          // past their buffer (data_off + data_len > buf_len)
   uint32_t slot_extra;    // bytes of room past each frame in its slot (nat64 4to6: 20)
   // optional (nullptr: not written), for the egress scatter:
   uint64_t *mb_dev;       // [n] device address of the rte_mbuf header (0: bad)

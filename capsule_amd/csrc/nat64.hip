@@ -59,7 +59,9 @@ constexpr uint32_t kFirstBit = 0x80000000u;  // pkt_slot: first packet of a new 
 constexpr uint32_t kLocalBit = 0x40000000u;  // pkt_slot: key first seen in this batch
 constexpr uint32_t kSlotMask = 0x3fffffffu;
 constexpr uint32_t kV4Addr = 0x017100cbu;    // 203.0.113.1 as LE dword of wire bytes
-constexpr uint32_t kDataRoom = 2048u;        // RTE_MBUF_DEFAULT_DATAROOM
+// The tailroom model of Mbuf::extend (mbuf.rs:225-233) is Nat64Args::room:
+// RTE_MBUF_DEFAULT_DATAROOM = 2048 for device batches; on the mbuf path the
+// host passes 65535 and the scatter checks each mbuf's real tailroom.
 constexpr uint32_t kNoRead = 0xffffff00u;    // > any arena length the ABI accepts
 
 __device__ __forceinline__ uint32_t sel3(uint32_t k, uint32_t a, uint32_t b, uint32_t c) {
@@ -107,7 +109,8 @@ struct V6 {
 // V6 from frame-relative dwords P[3..16] (bytes 12..67: the VLAN marker
 // through the TCP source port at QinQ depth); the checks follow the
 // reference nat_6to4 control flow in order.
-__device__ __forceinline__ void classify_dwords(const uint32_t (&P)[20], uint32_t len, V6 &v) {
+__device__ __forceinline__ void classify_dwords(const uint32_t (&P)[20], uint32_t len,
+                                                uint32_t room, V6 &v) {
   const uint32_t marker = be16_lo(P[3]);
   v.k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
   v.eth_len = 14u + 4u * v.k;
@@ -130,7 +133,7 @@ __device__ __forceinline__ void classify_dwords(const uint32_t (&P)[20], uint32_
   // v6.remove()? : shrink(eth_len, 40) cannot fail after a successful parse.
   // push::<Ipv4>()? : extend(eth_len, 20) needs 20 < tailroom (mbuf.rs:228).
   const uint32_t shrunk = len - 40u;
-  if (!(20u < (shrunk < kDataRoom ? kDataRoom - shrunk : 0u))) {
+  if (!(20u < (shrunk < room ? room - shrunk : 0u))) {
     v.st = CGPU_PKT_NOT_RESIZED;
     return;
   }
@@ -146,7 +149,7 @@ __device__ __forceinline__ void classify_dwords(const uint32_t (&P)[20], uint32_
 // batch-local key's representative frame with it): tail-safe dword loads of
 // bytes 0..79, zero past the frame end.
 __device__ __forceinline__ void classify(rsrc_t rs, uint32_t arena_len, uint32_t off,
-                                         uint32_t len, V6 &v) {
+                                         uint32_t len, uint32_t room, V6 &v) {
   constexpr int NW = 20;
   uint32_t P[NW];
   const uint32_t sh = off & 3u, base = off - sh;
@@ -157,7 +160,7 @@ __device__ __forceinline__ void classify(rsrc_t rs, uint32_t arena_len, uint32_t
     D[j] = (uint32_t)(4 * j) < need ? load4_tail(rs, base + 4u * j, arena_len) : 0u;
 #pragma unroll
   for (int j = 0; j < NW; ++j) P[j] = __builtin_amdgcn_alignbyte(D[j + 1], D[j], sh);
-  classify_dwords(P, len, v);
+  classify_dwords(P, len, room, v);
 }
 
 // key = (v6 src, tcp src port) = assigned_port(src, port) (main.rs:129,142-143)
@@ -264,7 +267,7 @@ __device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, rsrc_t rs, ui
       // its claimer may still be writing.
       const uint32_t rep = ref - 1u;
       V6 rv;
-      classify(rs, a.arena_len, a.off[rep], a.len[rep], rv);
+      classify(rs, a.arena_len, a.off[rep], a.len[rep], a.room, rv);
       uint32_t other[5];
       make_key(rv, other);
       match = key_eq(key, other);
@@ -556,7 +559,7 @@ __device__ __forceinline__ QuadDesc quad_desc(const Nat64Args &a, uint32_t i) {
 
 template <bool TO4>
 __device__ __forceinline__ void quad_modes(const Nat64Args &a, QuadDesc &d) {
-  const bool cand = TO4 ? (d.valid && d.len >= 74u) : (d.valid && d.len >= 54u && d.len < kDataRoom - 20u);
+  const bool cand = TO4 ? (d.valid && d.len >= 74u) : (d.valid && d.len >= 54u && d.len < a.room - 20u);
   d.nl = cand ? (TO4 ? d.len - 20u : d.len + 20u) : 0u;
   d.fast = !__ballot(cand && !((d.off & 3u) == 0u && (d.o_off & 3u) == 0u &&
                                (uint64_t)d.off + d.nl + 64u <= (uint64_t)a.arena_len &&
@@ -690,7 +693,7 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a
   uint32_t P[20];
   gather_header(Y, Y4, P);
   V6 v;
-  classify_dwords(P, d.len, v);
+  classify_dwords(P, d.len, a.room, v);
   // assigned_port (main.rs:41-53): lane 0 of the quad probes the table
   uint32_t slot = kNoSlot, port = 0xffffffffu;
   if (d.valid && g == 0u && v.disp == CGPU_ACT) {
@@ -931,7 +934,7 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_4to6_fused(Nat64Args a
     const uint64_t r = a.pm.rev[v.gw_port];
     if (r == ~0ull) {
       v.disp = CGPU_DROP;  // no mapping: Either::Drop
-    } else if (d.len >= kDataRoom - 20u) {  // push::<Ipv6>(): extend 40 needs 40 < tailroom
+    } else if (d.len >= a.room - 20u) {  // push::<Ipv6>(): extend 40 needs 40 < tailroom
       v.st = CGPU_PKT_NOT_RESIZED;
       v.disp = CGPU_ABORT;
     } else {

@@ -144,12 +144,28 @@ uint64_t or_flow_hash(int v6, const uint8_t *src, const uint8_t *dst, uint16_t s
 
 /* ---- a simulated single-segment rte_mbuf (core/src/dpdk/mbuf.rs) --------- */
 #define MBUF_HEADROOM 128u  /* RTE_PKTMBUF_HEADROOM */
-#define MBUF_BUF_LEN 2176u  /* 2048 data room + headroom (bindings_rustdoc.rs:561) */
+/* buf_len of the simulated mbufs: 2048 data room + headroom
+ * (bindings_rustdoc.rs:561) unless a test models a custom mempool
+ * (or_set_mbuf_data_room) */
+static uint32_t g_buf_len = 2176u;
+
+void or_set_mbuf_data_room(uint32_t room) { g_buf_len = MBUF_HEADROOM + room; }
 
 typedef struct {
-  uint8_t buf[MBUF_BUF_LEN];
+  uint8_t *buf; /* g_buf_len bytes */
   uint32_t data_off, data_len;
 } mbuf_t;
+
+static mbuf_t *mb_new(void) {
+  mbuf_t *m = (mbuf_t *)malloc(sizeof(mbuf_t));
+  m->buf = (uint8_t *)malloc(g_buf_len);
+  return m;
+}
+
+static void mb_free(mbuf_t *m) {
+  free(m->buf);
+  free(m);
+}
 
 static uint8_t *mb_data(mbuf_t *m, uint32_t off) { return m->buf + m->data_off + off; }
 
@@ -163,7 +179,7 @@ static int read_data(uint32_t data_len, uint32_t offset, uint32_t size_of, int b
 
 /* mbuf.rs:225-245 extend */
 static int mb_extend(mbuf_t *m, uint32_t offset, uint32_t len) {
-  uint32_t tailroom = MBUF_BUF_LEN - m->data_off - m->data_len;
+  uint32_t tailroom = g_buf_len - m->data_off - m->data_len;
   if (!(len > 0)) return -1;
   if (!(offset <= m->data_len)) return -1;
   if (!(len < tailroom)) return -1;
@@ -685,11 +701,11 @@ static int nat_4to6(or_portmap *pm, mbuf_t *m, uint8_t *status) {
 void or_nat64_4to6(or_portmap *pm, const uint8_t *arena, const uint32_t *off, const uint16_t *len,
                    uint32_t n, uint8_t *out_arena, const uint32_t *out_off, uint16_t *out_len,
                    uint8_t *disposition, uint8_t *status) {
-  mbuf_t *m = (mbuf_t *)malloc(sizeof(mbuf_t));
+  mbuf_t *m = mb_new();
   for (uint32_t i = 0; i < n; ++i) {
     m->data_off = MBUF_HEADROOM;
     m->data_len = len[i];
-    if (m->data_len > MBUF_BUF_LEN - MBUF_HEADROOM) m->data_len = MBUF_BUF_LEN - MBUF_HEADROOM;
+    if (m->data_len > g_buf_len - MBUF_HEADROOM) m->data_len = g_buf_len - MBUF_HEADROOM;
     memcpy(mb_data(m, 0), arena + off[i], m->data_len);
     int d = nat_4to6(pm, m, status + i);
     disposition[i] = (uint8_t)d;
@@ -700,17 +716,17 @@ void or_nat64_4to6(or_portmap *pm, const uint8_t *arena, const uint32_t *off, co
       out_len[i] = 0;
     }
   }
-  free(m);
+  mb_free(m);
 }
 
 void or_nat64_6to4(or_portmap *pm, const uint8_t *arena, const uint32_t *off, const uint16_t *len,
                    uint32_t n, uint8_t *out_arena, const uint32_t *out_off, uint16_t *out_len,
                    uint8_t *disposition, uint8_t *status) {
-  mbuf_t *m = (mbuf_t *)malloc(sizeof(mbuf_t));
+  mbuf_t *m = mb_new();
   for (uint32_t i = 0; i < n; ++i) {
     m->data_off = MBUF_HEADROOM;
     m->data_len = len[i];
-    if (m->data_len > MBUF_BUF_LEN - MBUF_HEADROOM) m->data_len = MBUF_BUF_LEN - MBUF_HEADROOM;
+    if (m->data_len > g_buf_len - MBUF_HEADROOM) m->data_len = g_buf_len - MBUF_HEADROOM;
     memcpy(mb_data(m, 0), arena + off[i], m->data_len);
     int d = nat_6to4(pm, m, status + i);
     disposition[i] = (uint8_t)d;
@@ -721,7 +737,7 @@ void or_nat64_6to4(or_portmap *pm, const uint8_t *arena, const uint32_t *off, co
       out_len[i] = 0;
     }
   }
-  free(m);
+  mb_free(m);
 }
 
 /* ---- group_by (core/src/batch/group_by.rs) ------------------------------ */

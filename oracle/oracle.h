@@ -60,6 +60,9 @@ or_portmap *or_portmap_new(uint16_t first_port);
 void or_portmap_free(or_portmap *pm);
 uint16_t or_portmap_next_port(const or_portmap *pm);
 uint32_t or_portmap_size(const or_portmap *pm);
+/* Data room of the simulated mbufs nat64 runs in (default 2048, DPDK's
+ * RTE_MBUF_DEFAULT_DATAROOM); a test of a custom mempool sets its own. */
+void or_set_mbuf_data_room(uint32_t room);
 void or_nat64_6to4(or_portmap *pm, const uint8_t *arena, const uint32_t *off, const uint16_t *len,
                    uint32_t n, uint8_t *out_arena, const uint32_t *out_off, uint16_t *out_len,
                    uint8_t *disposition, uint8_t *status);

@@ -42,6 +42,8 @@ def load(name="liboracle.so"):
     L.or_parse_batch_ext.argtypes = [vp, vp, vp, u32, u32, vp, vp, vp, vp, vp]
     L.or_multi_parse_udp.restype = u32
     L.or_multi_parse_udp.argtypes = [vp, vp, vp, u32]
+    L.or_set_mbuf_data_room.restype = None
+    L.or_set_mbuf_data_room.argtypes = [u32]
     L.or_portmap_new.restype = vp
     L.or_portmap_new.argtypes = [u16]
     L.or_portmap_free.restype = None
@@ -142,6 +144,20 @@ def group_by(key, n_groups, kind=0):
     off = np.zeros(n_groups + 1, np.uint32)
     lib().or_group_by(_p(key), kind, n, n_groups, _p(idx), _p(off))
     return idx, off
+
+
+class data_room:
+    """Context manager: the oracle's simulated mbufs get `room` bytes of data
+    room (a custom mempool) instead of DPDK's default 2048."""
+
+    def __init__(self, room):
+        self.room = room
+
+    def __enter__(self):
+        lib().or_set_mbuf_data_room(self.room)
+
+    def __exit__(self, *exc):
+        lib().or_set_mbuf_data_room(2048)
 
 
 class PortMap:

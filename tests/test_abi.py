@@ -80,3 +80,17 @@ def test_host_modules_import_without_gpu():
     from capsule_amd import packets, shards  # noqa: F401
 
     assert capsule_amd.packets is packets
+
+
+def test_plain_c_consumer_compiles_and_links(tmp_path):
+    """include/capsule_gpu.h as a C11 translation unit (the bindgen input):
+    record layouts and rte_mbuf offsets pinned by _Static_assert, every entry
+    point linked from libcapsule_gpu.so, host-only calls run."""
+    exe = tmp_path / "abi_check"
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-pedantic",
+                    f"-I{ROOT / 'include'}", str(ROOT / "tests" / "c" / "abi_check.c"),
+                    f"-L{N.LIB_PATH.parent}", "-lcapsule_gpu",
+                    f"-Wl,-rpath,{N.LIB_PATH.parent}", "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stderr)
+    assert r.stdout.startswith("abi ok: 20 entry points, not a UDP packet.")

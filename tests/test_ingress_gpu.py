@@ -161,3 +161,35 @@ def test_register_unregister_bookkeeping(ctx):
 def test_empty_burst(ctx):
     gm, gc, gh, _ = packets.parse_mbufs(ctx, np.zeros(0, np.uint64), ALL, N.INGRESS_ZERO_COPY)
     assert len(gm) == 0
+
+
+@pytest.mark.parametrize("ingress", MODES)
+def test_jumbo_mempool(ctx, ingress):
+    """A 9000-B data room with 9000-B frames: each frame needs more than the
+    2176-B slot the zero-copy gather sizes its arena for, so the arena grows
+    and the chunk is redone; results bit-exact either way."""
+    a, o, l = synth.uniform(700, kind=synth.V4_UDP, frame_len=9000, slot=9024, seed=6)
+    mem, mbufs = synth.mbuf_pool(a, o, l, room=9000)
+    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    try:
+        check(ctx, a, o, l, mbufs, ingress, fields=False)
+    finally:
+        reg.close()
+
+
+def test_zero_copy_rejects_frame_past_its_buffer(ctx):
+    """data_off + data_len > buf_len is no valid mbuf: the call fails."""
+    a, o, l = synth.imix(128, seed=8)
+    mem, mbufs = synth.mbuf_pool(a, o, l, room=2048)
+    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    try:
+        ob = int(mbufs[9]) - mem.ctypes.data
+        saved = mem[ob + 40: ob + 42].copy()
+        mem[ob + 40: ob + 42] = np.frombuffer(np.uint16(2049).tobytes(), np.uint8)
+        with pytest.raises(N.CgpuError) as e:
+            packets.parse_mbufs(ctx, mbufs, ALL, N.INGRESS_ZERO_COPY)
+        assert e.value.code == N.EINVAL
+        mem[ob + 40: ob + 42] = saved
+        check(ctx, a, o, l, mbufs, N.INGRESS_ZERO_COPY, fields=False)
+    finally:
+        reg.close()

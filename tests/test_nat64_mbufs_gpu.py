@@ -119,3 +119,71 @@ def test_nat64_mbufs_rejects_unregistered_and_empty(ctx):
     finally:
         reg.close()
         gw.close()
+
+
+def test_nat64_mbufs_bad_pointer_changes_nothing(ctx):
+    """A bad mbuf fails the call before anything is rewritten: every mbuf and
+    the port map are as they were -- for a one-chunk burst, for a burst of
+    two chunks (2^20 mbufs each) whose bad pointer is in the last one, and
+    for a frame that runs past its own buffer (data_off + data_len >
+    buf_len).  The intact burst then goes through."""
+    gw = packets.Nat64Gateway(ctx, capacity_log2=12)
+    a, o, l = synth.nat64_stream(4096, n_keys=300, seed=44)
+    mem, mbufs, reg = _pool(ctx, a, o, l, 2048)
+    before = mem.copy()
+    try:
+        for burst in (mbufs.copy(), np.tile(mbufs, 257)):
+            assert len(burst) in (4096, 4096 * 257)
+            burst[-1] = np.uint64(0x1000)  # outside every registered region
+            with pytest.raises(N.CgpuError) as e:
+                gw.nat_mbufs(burst, "6to4")
+            assert e.value.code == N.EINVAL
+            assert (mem == before).all()
+            assert gw.next_port() == 1025 and gw.size() == 0
+        ob = int(mbufs[7]) - mem.ctypes.data
+        mem[ob + 40: ob + 42] = np.frombuffer(np.uint16(2049).tobytes(), np.uint8)  # room 2048
+        with pytest.raises(N.CgpuError) as e:
+            gw.nat_mbufs(mbufs, "6to4")
+        assert e.value.code == N.EINVAL
+        mem[ob + 40: ob + 42] = before[ob + 40: ob + 42]
+        assert (mem == before).all() and gw.next_port() == 1025 and gw.size() == 0
+        disp, st = gw.nat_mbufs(mbufs, "6to4")
+        out, olen, odisp, ost = oracle_lib.PortMap().nat_6to4(a, o, l)
+        assert (disp == odisp).all() and (st == ost).all()
+        _check_mbufs(mem, mbufs, a, o, l, out, o, olen, disp)
+    finally:
+        reg.close()
+        gw.close()
+
+
+def test_nat64_mbufs_custom_data_room(ctx):
+    """A mempool with a 4096-B data room: 3000-B IPv6 frames (longer than
+    the 2176-B slots the gather assumes, so its arena grows) through 6to4,
+    and their 2980-B replies through 4to6, whose extend(20) fits the mbufs'
+    real tailroom -- a device batch, modelled on DPDK's 2048-B room, would
+    abort them (NotResized).  Oracle with the same data room."""
+    room = 4096
+    a, o, l = synth.nat64_stream(600, frame_len=3000, n_keys=40, seed=45)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=10)
+    pm = oracle_lib.PortMap()
+    mem, mbufs, reg = _pool(ctx, a, o, l, room)
+    try:
+        with oracle_lib.data_room(room):
+            disp, st = gw.nat_mbufs(mbufs, "6to4")
+            out, olen, odisp, ost = pm.nat_6to4(a, o, l)
+        assert (odisp == N.ACT).all() and (disp == odisp).all() and (st == ost).all()
+        _check_mbufs(mem, mbufs, a, o, l, out, o, olen, disp)
+    finally:
+        reg.close()
+    ra, ro, rl = synth.nat64_replies(out, o, olen)
+    mem2, mb2, reg2 = _pool(ctx, ra, ro, rl, room)
+    try:
+        with oracle_lib.data_room(room):
+            disp6, st6 = gw.nat_mbufs(mb2, "4to6")
+            out6, olen6, odisp6, ost6 = pm.nat_4to6(ra, ro, rl, ro + 0, len(ra))
+        assert (odisp6 == N.ACT).all() and (olen6 == 3000).all()
+        assert (disp6 == odisp6).all() and (st6 == ost6).all()
+        _check_mbufs(mem2, mb2, ra, ro, rl, out6, ro, olen6, disp6)
+    finally:
+        reg2.close()
+        gw.close()
