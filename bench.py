@@ -77,8 +77,16 @@ def make_workload(cfg, seed):
                     algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame="IMIX")
     if cfg == "nat64":
         arena, off, ln = synth.nat64_stream(n, seed=seed)
-        desc = "1M x 256B IPv6/TCP -> IPv4 6to4 rewrite + TCP/IPv4 checksums (examples/nat64)"
+        desc = ("1M x 256B IPv6/TCP -> IPv4 6to4 rewrite + TCP/IPv4 checksums (examples/nat64), "
+                "236-B output frames packed back to back")
+        # The egress buffer is packed (a TX ring / DMA-out image): with the
+        # frames left in 256-B slots every frame's last output line would be
+        # written partially.
+        new_len = ln.astype(np.int64) - 20
+        out_off = np.zeros(n, np.int64)
+        out_off[1:] = np.cumsum(new_len)[:-1]
         return dict(arena=arena, off=off, len=ln, flags=0, kind="nat64", desc=desc,
+                    out_off=out_off.astype(np.uint32), out_size=int(new_len.sum()) + 64,
                     algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame="256B")
     if cfg == "nat64_4to6":
         # the v6 stream that populates the port map; the timed replies are
@@ -252,6 +260,7 @@ SIZES = ("parse256", "parse1500", "imix", "imix_csum", "nat64")
 # BASELINE config 5: IMIX shards, one per GPU (the `shards` object)
 SHARD_CONFIG = "imix"
 MIN_WARM_S = 0.06  # device time of warm-up before any timed region (steady clocks)
+PORTMAP_LOG2 = int(os.environ.get("CGPU_BENCH_PORTMAP_LOG2", "20"))  # Nat64Gateway default
 
 
 def pmc_traffic(cfg):
@@ -299,10 +308,17 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None):
                                            stream) for k in range(2 * copies)]
     else:
         direction = "4to6" if gw is not None else "6to4"
-        gw = gw or packets.Nat64Gateway(ctx, capacity_log2=17)
-        outs = [(torch.empty_like(b.arena), b.off, torch.empty(n, dtype=torch.int16, device=dev),
-                 torch.empty(n, dtype=torch.uint8, device=dev),
-                 torch.empty(n, dtype=torch.uint8, device=dev)) for b in batches[:2]]
+        gw = gw or packets.Nat64Gateway(ctx, capacity_log2=PORTMAP_LOG2)
+        if "out_off" in w:
+            oo = torch.from_numpy(w["out_off"].view(np.int32)).to(dev)
+            outs = [(torch.empty(w["out_size"], dtype=torch.uint8, device=dev), oo,
+                     torch.empty(n, dtype=torch.int16, device=dev),
+                     torch.empty(n, dtype=torch.uint8, device=dev),
+                     torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(2)]
+        else:
+            outs = [(torch.empty_like(b.arena), b.off, torch.empty(n, dtype=torch.int16, device=dev),
+                     torch.empty(n, dtype=torch.uint8, device=dev),
+                     torch.empty(n, dtype=torch.uint8, device=dev)) for b in batches[:2]]
         launchers = [packets.Nat64Launcher(gw, batches[k % copies], outs[k & 1], stream,
                                            direction) for k in range(2 * copies)]
     cycle = len(launchers)

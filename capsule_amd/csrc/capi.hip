@@ -86,7 +86,6 @@ struct cgpu_portmap {
   uint64_t *lookback = nullptr;
   void *rec_h = nullptr;  // deferred frames' header records
   void *rec_b = nullptr;
-  uint32_t *defer = nullptr;
   uint32_t scratch_n = 0;
   uint32_t calls = 0;  // 6to4 calls: parity of the deferred-list counter
   // the stream of the latest call: calls on one map are stream-ordered
@@ -614,8 +613,8 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
     const size_t o_sums = align_up(4ull * in->n, 256);
     const size_t o_rech = o_sums + align_up(8ull * nb, 256);
     const size_t o_recb = o_rech + align_up(16ull * in->n, 256);
-    const size_t o_defer = o_recb + align_up(8ull * in->n, 256);
-    if (hipMalloc(&m, o_defer + 4ull * in->n + 256) != hipSuccess) return fail(CGPU_ENOMEM);
+    const size_t o_end = o_recb + align_up(8ull * in->n, 256);
+    if (hipMalloc(&m, o_end + 256) != hipSuccess) return fail(CGPU_ENOMEM);
     pm->pkt_slot = (uint32_t *)m;
     pm->lookback = (uint64_t *)((uint8_t *)m + o_sums);
     // status 0 = "not published" in every epoch
@@ -623,7 +622,6 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
       return fail(CGPU_EIO);
     pm->rec_h = (uint8_t *)m + o_rech;
     pm->rec_b = (uint8_t *)m + o_recb;
-    pm->defer = (uint32_t *)((uint8_t *)m + o_defer);
     pm->scratch_n = in->n;
   }
   cgpu::Nat64Args a;
@@ -643,7 +641,6 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   a.epoch = pm->calls;
   a.rec_h = (cgpu::u32x4 *)pm->rec_h;
   a.rec_b = (uint2 *)pm->rec_b;
-  a.defer = pm->defer;
   a.par = pm->calls & 1u;
   a.room = pm->room;
   a.pm = pm->dev;

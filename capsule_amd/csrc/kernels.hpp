@@ -48,7 +48,8 @@ struct PortSlot {
 struct PortMapDev {
   PortSlot *slots;  // [cap]
   uint64_t *rev;    // [65536]: (first ordinal << 32 | slot), ~0 = none (ADDR_MAP, main.rs:38)
-  uint32_t *state;  // [9]: next_port, entries, -, -, deferred[2], chunk tickets[2], batch new keys
+  uint32_t *state;  // [11]: next_port, entries, -, -, deferred[2], chunk tickets[2],
+                    // batch new keys, chunks ordered[2]
   uint32_t cap_mask;
 };
 
@@ -69,8 +70,7 @@ struct Nat64Args {
   uint32_t epoch;        // 6to4 call number (look-back words of other calls are stale)
   u32x4 *rec_h;          // scratch [n]: deferred 6to4 frames' IPv4 header dwords 0..3
   uint2 *rec_b;          // scratch [n]: header dword 4, VLAN depth
-  uint32_t *defer;       // scratch [n]: indices of the deferred 6to4 frames
-  uint32_t par;          // call parity: selects the deferred-list counter state[4 + par]
+  uint32_t par;          // call parity: selects the per-call counters state[4/6/9 + par]
   uint32_t room;         // data room of Mbuf::extend's tailroom model (mbuf.rs:225-233):
                          // 2048 for device batches; 65535 on the mbuf path, whose
                          // scatter checks each mbuf's real tailroom instead

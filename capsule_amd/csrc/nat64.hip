@@ -28,16 +28,14 @@
 //     span with v_sad_u16; the quad reduces; the lane holding the TCP
 //     checksum field stores it last.
 // A 6to4 frame whose key is not yet committed (first seen in this batch)
-// needs the batch-wide first-seen order, so the fused kernel defers it: its
-// header record goes to global scratch and its index to a deferred list, and
-//   K2 order   per 256-packet chunk: count the first packets of new keys,
-//              decoupled look-back scan of the counts, port = NEXT_PORT +
-//              ordinal (ballot/popcount rank within the chunk)
-//   K5 rewrite the deferred frames (the same quad rewrite, list-driven),
-//              commit the keys, advance NEXT_PORT
-// finish them.  When no key is new (the steady state) K2 and K5 see an
-// empty deferred list and return at once.  Kernel boundaries are the only
-// cross-workgroup hand-offs besides device-scope atomics on the table.
+// needs the batch-wide first-seen order, so the fused kernel defers it (its
+// header record goes to global scratch) and a tail kernel finishes it: per
+// 256-packet chunk it counts the first packets of new keys, scans the counts
+// with a decoupled look-back, assigns port = NEXT_PORT + ordinal, commits
+// the keys, and rewrites the chunk's deferred frames.  When no key is new
+// (the steady state) the tail returns at once.  The fused kernel takes the
+// rows path (four whole frames per load and store instruction, see below) when a wave's
+// frames allow it and the quad path otherwise.
 #include "capsule_gpu.h"
 #include "device_common.hpp"
 #include "kernels.hpp"
@@ -47,6 +45,12 @@ namespace cgpu {
 namespace {
 
 constexpr uint32_t kBlock = 256;
+// cache policy bits of the frame-stream loads and stores (A/B knob; 0 =
+// default policy)
+#ifndef CGPU_NAT64_AUX
+#define CGPU_NAT64_AUX 0
+#endif
+constexpr int kAux = CGPU_NAT64_AUX;
 #ifndef CGPU_NAT64_WPE
 #define CGPU_NAT64_WPE 1
 #endif
@@ -55,9 +59,9 @@ constexpr uint32_t kFG = 4u;                 // lanes per frame in the rewrite p
 constexpr uint32_t kFJ = 16u / kFG;          // 16-B chunks per lane per 256-B pass
 constexpr uint32_t kNow = 4u;                // record info bit: rewrite in the fused kernel
 constexpr uint32_t kNoSlot = 0xffffffffu;
-constexpr uint32_t kFirstBit = 0x80000000u;  // pkt_slot: first packet of a new key
 constexpr uint32_t kLocalBit = 0x40000000u;  // pkt_slot: key first seen in this batch
 constexpr uint32_t kSlotMask = 0x3fffffffu;
+constexpr uint32_t kNoPort = 0xffffffffu;       // PortSlot::w[6] of a key not yet ordered
 constexpr uint32_t kV4Addr = 0x017100cbu;    // 203.0.113.1 as LE dword of wire bytes
 // The tailroom model of Mbuf::extend (mbuf.rs:225-233) is Nat64Args::room:
 // RTE_MBUF_DEFAULT_DATAROOM = 2048 for device batches; on the mbuf path the
@@ -196,14 +200,14 @@ __device__ __forceinline__ void store_out(rsrc_t ors, uint8_t *out_arena, uint32
                                           uint32_t c, u32x4 v, uint32_t len, bool aligned) {
   const uint32_t o = out_base + 16u * c;
   if (aligned && 16u * c + 16u <= len) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)o, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)o, 0, kAux);
     return;
   }
 #pragma unroll
   for (uint32_t t = 0; t < 4u; ++t) {
     const uint32_t b = 16u * c + 4u * t;
     if (aligned && b + 4u <= len) {
-      __builtin_amdgcn_raw_buffer_store_b32(v[t], ors, (int)(o + 4u * t), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(v[t], ors, (int)(o + 4u * t), 0, kAux);
     } else {
       for (uint32_t q = 0; q < 4u; ++q)
         if (b + q < len) out_arena[o + 4u * t + q] = (uint8_t)(v[t] >> (8u * q));
@@ -233,18 +237,19 @@ __device__ __forceinline__ void ipv4_header(const V6 &v, uint32_t len, uint32_t 
 // (kNoSlot: table full) and, for a key committed by an earlier batch, its
 // port; a key first seen in this batch is claimed (CAS) or joined, and its
 // first packet index recorded (atomicMin) for K2..K4.
-__device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, rsrc_t rs, uint32_t i, const V6 &v,
-                                               uint32_t &port) {
-  uint32_t key[5];
-  make_key(v, key);
-  uint32_t h = key_hash(key) & a.pm.cap_mask;
+__device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, rsrc_t rs, uint32_t i,
+                                                  const uint32_t (&key)[5], uint32_t h, u32x4 s0,
+                                                  u32x4 s1, uint32_t &port) {
   port = 0xffffffffu;
   for (uint32_t probe = 0; probe <= a.pm.cap_mask; ++probe) {
     // Keys committed by earlier batches are matched from one 32-B slot
     // load; an empty slot is claimed with a CAS.  refs only ever go
     // 0 -> (i + 1) -> kPersist, so a stale 0 just leads to the CAS.
-    const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
-    const u32x4 s0 = sp[0], s1 = sp[1];
+    if (probe != 0u) {  // the first slot was loaded by the caller
+      const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
+      s0 = sp[0];
+      s1 = sp[1];
+    }
     uint32_t ref = s0[0];
     bool claimed = false;
     if (ref == 0u) {
@@ -257,6 +262,7 @@ __device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, rsrc_t rs, ui
 #pragma unroll
       for (int j = 0; j < 4; ++j) a.pm.slots[h].w[1 + j] = key[j];
       a.pm.slots[h].w[5] = key[4];
+      a.pm.slots[h].w[6] = kNoPort;  // assigned by the tail kernel's order step
     } else if (ref & kPersist) {
       const uint32_t other[5] = {s0[1], s0[2], s0[3], s1[0], s1[1]};
       match = key_eq(key, other);
@@ -280,6 +286,19 @@ __device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, rsrc_t rs, ui
     h = (h + 1u) & a.pm.cap_mask;
   }
   return kNoSlot;
+}
+
+// assigned_port (main.rs:41-53) lookup for frame i: returns the table slot
+// (kNoSlot: table full) and, for a key committed by an earlier batch, its
+// port; a key first seen in this batch is claimed (CAS) or joined, and its
+// first packet index recorded (atomicMin) for K2..K4.
+__device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, rsrc_t rs, uint32_t i, const V6 &v,
+                                               uint32_t &port) {
+  uint32_t key[5];
+  make_key(v, key);
+  const uint32_t h = key_hash(key) & a.pm.cap_mask;
+  const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
+  return probe_port_at(a, rs, i, key, h, sp[0], sp[1], port);
 }
 
 // ---- the rewrite of one frame by its quad (fused kernels and K5) -------------
@@ -327,25 +346,25 @@ __device__ __forceinline__ void store_chunk(rsrc_t ors, uint8_t *out_arena, uint
     return;
   }
   if (b0 + 16u <= nl) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(o_off + b0), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(o_off + b0), 0, kAux);
   } else if (b0 < nl) {
     // The partial last chunk, r = 1..15 bytes: its whole dwords in one
     // b32/b64/b96 store, then a b16 and/or b8 for the trailing bytes.  With
     // a wave-uniform frame length only one of the paths below is issued.
     const uint32_t r = nl - b0, d = r >> 2, tb = r & 3u, o = o_off + b0;
     if (d == 3u) {
-      __builtin_amdgcn_raw_buffer_store_b96(u32x3{v[0], v[1], v[2]}, ors, (int)o, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b96(u32x3{v[0], v[1], v[2]}, ors, (int)o, 0, kAux);
     } else if (d == 2u) {
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{v[0], v[1]}, ors, (int)o, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{v[0], v[1]}, ors, (int)o, 0, kAux);
     } else if (d == 1u) {
-      __builtin_amdgcn_raw_buffer_store_b32(v[0], ors, (int)o, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(v[0], ors, (int)o, 0, kAux);
     }
     if (tb != 0u) {
       const uint32_t w = d == 0u ? v[0] : (d == 1u ? v[1] : (d == 2u ? v[2] : v[3]));
       const uint32_t ob = o + 4u * d;
-      if (tb >= 2u) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)w, ors, (int)ob, 0, 0);
+      if (tb >= 2u) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)w, ors, (int)ob, 0, kAux);
       if (tb & 1u) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> (8u * (tb & 2u))), ors,
-                                                       (int)(ob + (tb & 2u)), 0, 0);
+                                                       (int)(ob + (tb & 2u)), 0, kAux);
     }
   }
 }
@@ -450,7 +469,7 @@ __device__ __forceinline__ void rewrite_frame(const Nat64Args &a, rsrc_t rs, rsr
       if (PRE && q == 0u) {
         o[j] = pre[j];
       } else if (FAST) {
-        o[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(need ? chunk_src<TO4>(f.in_off, c) : kNoRead), 0, 0);
+        o[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(need ? chunk_src<TO4>(f.in_off, c) : kNoRead), 0, kAux);
       } else {
         o[j] = u32x4{0u, 0u, 0u, 0u};
         if (need) o[j] = load_in(rs, a.arena_len, chunk_src<TO4>(f.in_off, c), in_al_wave);
@@ -504,8 +523,8 @@ __device__ __forceinline__ void header_loads(rsrc_t rs, uint32_t arena_len, uint
   Y = u32x4{0u, 0u, 0u, 0u};
   Y4 = u32x4{0u, 0u, 0u, 0u};
   if (hdr_fast) {
-    Y = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(valid ? off + 16u * g : kNoRead), 0, 0);
-    Y4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(valid && g == 0u ? off + 64u : kNoRead), 0, 0);
+    Y = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(valid ? off + 16u * g : kNoRead), 0, kAux);
+    Y4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(valid && g == 0u ? off + 64u : kNoRead), 0, kAux);
   } else if (valid) {
     Y = load_in(rs, arena_len, off + 16u * g, al_wave);
     if (g == 0u) Y4 = load_in(rs, arena_len, off + 64u, al_wave);
@@ -534,7 +553,7 @@ __device__ __forceinline__ void pass0_loads(rsrc_t rs, uint32_t off, uint32_t nl
   for (uint32_t j = 0; j < kFJ; ++j) {
     const uint32_t c = kFG * j + g;
     X[j] = u32x4{0u, 0u, 0u, 0u};
-    if (fast) X[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * c < nl ? chunk_src<TO4>(off, c) : kNoRead), 0, 0);
+    if (fast) X[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * c < nl ? chunk_src<TO4>(off, c) : kNoRead), 0, kAux);
   }
 }
 
@@ -602,12 +621,12 @@ __device__ __forceinline__ void aligned_loads(rsrc_t rs, uint32_t in_off, uint32
     const uint32_t c = 16u * q + kFG * j + g;
     // 6to4: chunk c's load also serves output chunk c - 1's last dword
     const bool need = TO4 ? 16u * c < nl + 4u : 16u * c < nl;
-    A[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(need ? aligned_src<TO4>(in_off, c) : kNoRead), 0, 0);
+    A[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(need ? aligned_src<TO4>(in_off, c) : kNoRead), 0, kAux);
   }
   E = 0u;
   if (TO4) {
     const uint32_t c = 16u * q + 15u;
-    E = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(g == 3u && 16u * c < nl ? in_off + 16u * (c + 2u) : kNoRead), 0, 0);
+    E = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(g == 3u && 16u * c < nl ? in_off + 16u * (c + 2u) : kNoRead), 0, kAux);
   }
 }
 
@@ -679,11 +698,22 @@ __device__ __forceinline__ void rewrite_quad(const Nat64Args &a, rsrc_t rs, rsrc
   else rewrite_frame<TO4, false, false>(a, rs, ors, g, f, d.al_wave, X);
 }
 
-__global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a) {
-  const uint32_t lane = threadIdx.x & 63u, g = threadIdx.x & (kFG - 1u);
-  const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
-  const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
-  QuadDesc d = quad_desc<true>(a, blockIdx.x * (kBlock / kFG) + threadIdx.x / kFG);
+// Count the wave's deferred frames (flag set in their lane), one atomic per
+// wave: the tail kernel returns at once when the count is 0.
+__device__ __forceinline__ void defer_append(const Nat64Args &a, uint32_t lane, bool flag,
+                                             uint32_t i) {
+  (void)i;
+  const uint64_t dm = __ballot(flag);
+  if (!dm) return;
+  if (lane == (uint32_t)__builtin_ctzll(dm)) atomicAdd(&a.pm.state[4u + a.par], (uint32_t)__popcll(dm));
+}
+
+// The general path: one quad per frame (any alignment, any length); `i` is
+// the quad's frame, lane the wave lane.
+__device__ __forceinline__ void quad_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t ors, uint32_t i,
+                                          uint32_t lane) {
+  const uint32_t g = lane & (kFG - 1u);
+  QuadDesc d = quad_desc<true>(a, i);
   quad_modes<true>(a, d);
   const bool al16 = d.fast && !__ballot(d.nl != 0u && (d.off & 15u) != 0u);
   u32x4 X[kFJ], Y, Y4;
@@ -725,17 +755,7 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a
     a.disposition[d.i] = (uint8_t)v.disp;
     a.status[d.i] = (uint8_t)v.st;
   }
-  // append the deferred frames to the list (one atomic per wave)
-  const uint64_t dm = __ballot(deferred && g == 0u);
-  if (dm) {
-    const uint32_t leader = (uint32_t)__builtin_ctzll(dm);
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&a.pm.state[4u + a.par], (uint32_t)__popcll(dm));
-    base = __shfl(base, (int)leader);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
-    if (deferred && g == 0u) a.defer[base + rank] = d.i;
-  }
+  defer_append(a, lane, deferred && g == 0u, d.i);
 #ifndef CGPU_NAT64_ABL_NOREWRITE  // timing ablation only: classify + probe alone
   if (now) {
     FrameRec f;
@@ -753,6 +773,267 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a
 #endif
 }
 
+// ---- the rows path: F frames per wave ---------------------------------------
+// When every frame of a wave is 16-B aligned in the input, dword-aligned in
+// the output and at most 256 B long (one input pass), the wave moves its frames in rows of 16 lanes, four
+// whole frames per load and store instruction (full lines), and decides per
+// frame in one lane:
+//   A. each lane loads the first 96 B of its own frame, then row j loads
+//      frame 4r + j in round r, lane l its 16-B chunk l; while those loads
+//      are in flight each lane classifies its frame, probes the port map
+//      (the probe's latency hides behind the row loads) and builds output
+//      bytes 0..63 (Ethernet, the IPv4 header, the start of the rewritten TCP
+//      header) and their part of the TCP sum into a wave-private LDS record;
+//   B. the payload moved by 20 B (in(l+1).yzw and in(l+2).x by DPP row
+//      shifts) and its TCP sum (a DPP row reduction), while the port-map
+//      probes are in flight; then row j writes frame 4r + j in one store
+//      instruction (whole lines): lanes 0-3 the chunks built in A, lanes
+//      4-14 the payload, lane 3 with the TCP checksum patched in.
+// Wave-uniform specialisations: no VLAN tag in the wave (static header
+// layout), one output length for the wave (per-lane chunk masks computed
+// once).
+constexpr uint32_t kRowW = 20;  // LDS dwords per frame record
+#ifndef CGPU_NAT64_ROW_FRAMES
+#define CGPU_NAT64_ROW_FRAMES 32
+#endif
+constexpr uint32_t kRowFrames = CGPU_NAT64_ROW_FRAMES;  // frames per wave (32 or 64)
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dppz(uint32_t v) {  // lanes without a source get 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, true);
+}
+constexpr int kRowShl1 = 0x101, kRowShl2 = 0x102;
+constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
+
+// Record layout (dwords of the frame's LDS slot, written in phase A):
+//   0..15  output bytes 0..63 (TCP checksum field zero)
+//   16     output length if the frame is finished here, else 0
+//   17     TCP sum (LE words) of the span bytes among output bytes 0..63
+//   18     v4 pseudo-header sum | VLAN depth << 16
+//   19     output offset
+template <bool K0>
+__device__ __forceinline__ void rows_build(const uint32_t (&D)[24], const uint32_t (&H)[10],
+                                           uint32_t k, uint32_t port_be, uint32_t nl,
+                                           uint32_t (&O)[16], uint32_t &acc) {
+  acc = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    const int r = w - (K0 ? 0 : (int)k);
+    const uint32_t x = w < 8 ? D[w] : D[w + 5];  // output bytes >= 32: input + 20
+    const uint32_t d = out_dword<true>(r, x, H, port_be);
+    uint32_t m = r < 8 ? 0u : (r == 8 ? 0xffff0000u : 0xffffffffu);
+    m &= range_mask(4u * (uint32_t)w, 0u, nl);
+    acc = sad16(d & m, acc);
+    O[w] = d;
+  }
+}
+
+// Row-path cache policy of the frame loads and of the whole-row stores
+// (A/B knob: 2 = nontemporal; only the rows path writes whole lines per
+// instruction, so only it can use nontemporal stores without splitting them)
+#ifndef CGPU_NAT64_ROW_AUX
+#define CGPU_NAT64_ROW_AUX 0
+#endif
+#ifndef CGPU_NAT64_ROW_LD_AUX
+#define CGPU_NAT64_ROW_LD_AUX 0
+#endif
+constexpr int kRowAux = CGPU_NAT64_ROW_AUX;       // whole-row stores
+constexpr int kRowLdAux = CGPU_NAT64_ROW_LD_AUX;  // frame loads
+
+// B1: the payload of every round -- output chunks 4.. realigned in place
+// (X[r] becomes output chunk l of frame 4r + row) and their TCP sum, reduced
+// over the row into lane 15, which leaves it in the frame's record (rec[17]).
+// Needs only the frames' lengths, not the port map, so it runs while the
+// probes are in flight.
+template <bool UNI>
+__device__ __forceinline__ void rows_payload(u32x4 (&X)[kRowFrames / 4], uint32_t *lds, uint32_t row,
+                                             uint32_t l, uint32_t nl0) {
+  // UNI: every ACT frame of the wave has output length nl0, so this lane's
+  // byte masks are the same in every round
+  u32x4 M0;
+#pragma unroll
+  for (uint32_t t = 0; t < 4u; ++t) M0[t] = range_mask(16u * l + 4u * t, 0u, nl0);
+#pragma unroll
+  for (uint32_t r = 0; r < kRowFrames / 4u; ++r) {
+    uint32_t *fr = lds + (4u * r + row) * kRowW;
+    const uint32_t fnl = fr[16];
+    if (!__ballot(fnl != 0u)) continue;  // no ACT frame in this round
+    const u32x4 A = X[r];
+    u32x4 o;
+    o[0] = dppz<kRowShl1>(A[1]);
+    o[1] = dppz<kRowShl1>(A[2]);
+    o[2] = dppz<kRowShl1>(A[3]);
+    o[3] = dppz<kRowShl2>(A[0]);
+    uint32_t acc = 0;
+    if (l >= 4u) {
+#pragma unroll
+      for (uint32_t t = 0; t < 4u; ++t)
+        acc = sad16(o[t] & (UNI ? M0[t] : range_mask(16u * l + 4u * t, 0u, fnl)), acc);
+    }
+    acc += dppz<kRowShr1>(acc);
+    acc += dppz<kRowShr2>(acc);
+    acc += dppz<kRowShr4>(acc);
+    acc += dppz<kRowShr8>(acc);
+    if (l == 15u) fr[17] = acc;
+    X[r] = o;
+  }
+}
+
+// B2: row j writes frame 4r + j in one store instruction (whole lines):
+// lanes 0-3 the chunks built in A, lanes 4.. the realigned payload; lane 3
+// patches the TCP checksum into its chunk.
+__device__ __forceinline__ void rows_store(const Nat64Args &a, rsrc_t ors, const u32x4 (&X)[kRowFrames / 4],
+                                           const uint32_t *lds, uint32_t row, uint32_t l) {
+#pragma unroll
+  for (uint32_t r = 0; r < kRowFrames / 4u; ++r) {
+    const uint32_t *fr = lds + (4u * r + row) * kRowW;
+    const u32x4 meta = *reinterpret_cast<const u32x4 *>(fr + 16);
+    const uint32_t fnl = meta[0];
+    if (!__ballot(fnl != 0u)) continue;  // no frame of this round is finished here
+    const u32x4 hc = *reinterpret_cast<const u32x4 *>(fr + 4u * (l & 3u));
+    u32x4 o = l < 4u ? hc : X[r];
+    if (l == 3u) {
+      const uint32_t fk = meta[2] >> 16, fph = meta[2] & 0xffffu;
+      const uint32_t tcp_c = (~fold32(fph + swap16(fold32(meta[1])))) & 0xffffu;
+#pragma unroll
+      for (uint32_t t = 0; t < 4u; ++t)
+        if (t == fk) o[t] |= swap16(tcp_c) << 16;
+    }
+    if (fnl != 0u) {
+      const uint32_t b0 = 16u * l;
+      if (b0 + 16u <= fnl) __builtin_amdgcn_raw_buffer_store_b128(o, ors, (int)(meta[3] + b0), 0, kRowAux);
+      else if (b0 < fnl) store_chunk<true>(ors, a.out_arena, meta[3], l, o, fnl);
+    }
+  }
+}
+
+__device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t ors, uint32_t base,
+                                          uint32_t lane, uint32_t *lds) {
+  constexpr uint32_t R = kRowFrames / 4u;  // rounds
+  const uint32_t i = base + lane;
+  const bool mine = lane < kRowFrames;
+  const bool valid = mine && i < a.n;
+  const uint32_t off = valid ? a.off[i] : 0u;
+  const uint32_t len = valid ? (uint32_t)a.len[i] : 0u;
+  const uint32_t o_off = valid ? a.out_off[i] : 0u;
+  // 16-B aligned input (aligned loads, DPP realignment), dword-aligned output
+  // (b128 stores at any dword: packed output frames stay on this path)
+  if (__ballot(valid && ((off & 15u) != 0u || (o_off & 3u) != 0u || len > 256u))) return false;
+  const uint32_t row = lane >> 4, l = lane & 15u;
+  // A1: this lane's own frame, input bytes 0..95, for the classification
+  uint32_t D[24];
+#pragma unroll
+  for (uint32_t m = 0; m < 6u; ++m) {
+    const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * m < len ? off + 16u * m : kNoRead), 0, kRowLdAux);
+    D[4 * m] = t[0]; D[4 * m + 1] = t[1]; D[4 * m + 2] = t[2]; D[4 * m + 3] = t[3];
+  }
+  // A2: the frames in rows, four whole frames per load instruction; in
+  // flight while the headers are classified and the port map is probed
+  u32x4 X[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t f = 4u * r + row;
+    const uint32_t fo = __shfl(off, (int)f), fl = __shfl(len, (int)f);
+    X[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * l < fl ? fo + 16u * l : kNoRead), 0, kRowLdAux);
+  }
+  uint32_t *rec = lds + (mine ? lane : 0u) * kRowW;
+  // A3: the reference control flow; the first port-map slot of the key is
+  // loaded now and examined after B1
+  uint32_t P[20];
+#pragma unroll
+  for (int j = 0; j < 20; ++j) P[j] = D[j];
+  V6 v;
+  classify_dwords(P, len, a.room, v);
+  const bool act0 = valid && v.disp == CGPU_ACT;
+  uint32_t key[5];
+  make_key(v, key);
+  const uint32_t h = key_hash(key) & a.pm.cap_mask;
+  u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
+#ifndef CGPU_NAT64_ABL_NOPROBE
+  if (act0) {
+    const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
+    s0 = sp[0];
+    s1 = sp[1];
+  }
+#endif
+  const uint32_t nl = len - 20u;  // meaningful for ACT frames
+  if (mine) {
+    rec[16] = act0 ? nl : 0u;
+    rec[19] = o_off;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // B1: realign and sum the payload of every round (port-independent)
+  const uint32_t nl0 = __shfl(nl, (int)(__builtin_ctzll(__ballot(act0) | (1ull << 63))));
+  if (!__ballot(act0 && nl != nl0)) rows_payload<true>(X, lds, row, l, nl0);
+  else rows_payload<false>(X, lds, row, l, nl0);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // A4: assigned_port (main.rs:41-53), the IPv4 header
+  uint32_t slot = kNoSlot, port = 0xffffffffu;
+  if (act0) {
+#ifdef CGPU_NAT64_ABL_NOPROBE
+    slot = 0u;
+    port = 1025u;
+#else
+    slot = probe_port_at(a, rs, i, key, h, s0, s1, port);
+#endif
+  }
+  if (v.disp == CGPU_ACT && slot == kNoSlot) {
+    v.disp = CGPU_ABORT;
+    v.st = CGPU_PKT_TABLE_FULL;
+  }
+  const bool act = valid && v.disp == CGPU_ACT;
+  uint32_t H[10];
+  ipv4_header(v, len, reinterpret_cast<uint32_t(&)[5]>(H));
+#pragma unroll
+  for (int j = 5; j < 10; ++j) H[j] = 0u;
+  const bool now = act && port != 0xffffffffu;
+  const bool deferred = act && !now;
+  if (valid) {
+    if (deferred) {
+      a.rec_h[i] = u32x4{H[0], H[1], H[2], H[3]};
+      a.rec_b[i] = make_uint2(H[4], v.k);
+    }
+    a.out_len[i] = now ? (uint16_t)nl : 0;
+    a.pkt_slot[i] = now ? kNoSlot : slot;
+    a.disposition[i] = (uint8_t)v.disp;
+    a.status[i] = (uint8_t)v.st;
+  }
+  defer_append(a, lane, deferred, i);
+  // A5: output bytes 0..63 and their share of the TCP sum; the record
+  const uint32_t k = v.k, port_be = swap16(port & 0xffffu);
+  uint32_t O[16], accA;
+  if (!__ballot(now && k != 0u)) rows_build<true>(D, H, k, port_be, nl, O, accA);
+  else rows_build<false>(D, H, k, port_be, nl, O, accA);
+  const uint32_t span = (nl - (34u + 4u * k)) & 0xffffu;
+  const uint32_t dst = be32(H[4]);
+  const uint32_t ph = fold32(0xcb00u + 0x7101u + (dst >> 16) + (dst & 0xffffu) + 6u + span);
+  if (mine) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      *reinterpret_cast<u32x4 *>(rec + 4 * m) = u32x4{O[4 * m], O[4 * m + 1], O[4 * m + 2], O[4 * m + 3]};
+    const uint32_t payload = rec[17];
+    *reinterpret_cast<u32x4 *>(rec + 16) =
+        u32x4{now ? nl : 0u, payload + accA, ph | (k << 16), o_off};
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#ifndef CGPU_NAT64_ABL_NOREWRITE
+  rows_store(a, ors, X, lds, row, l);
+#endif
+  return true;
+}
+
+__global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a) {
+  __shared__ uint32_t lds[kBlock / 64][kRowFrames * kRowW];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t base = (blockIdx.x * (kBlock / 64u) + wave) * kRowFrames;
+  if (base >= a.n) return;  // wave-uniform
+  const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
+  const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
+  if (rows_6to4(a, rs, ors, base, lane, lds[wave])) return;
+  // the general path: rounds of 16 frames, a quad per frame
+  for (uint32_t q = 0; q < kRowFrames / 16u; ++q) quad_6to4(a, rs, ors, base + 16u * q + lane / 4u, lane);
+}
+
 // Only packets whose key was first seen in this batch touch the table here.
 __device__ __forceinline__ bool is_first_new(const Nat64Args &a, uint32_t i) {
   const uint32_t ps = a.pkt_slot[i];
@@ -760,108 +1041,141 @@ __device__ __forceinline__ bool is_first_new(const Nat64Args &a, uint32_t i) {
   return a.pm.slots[ps & kSlotMask].w[7] == i;
 }
 
-// ---- K2: count, scan and assign in one pass (decoupled look-back) ---------
-// Chunk b (256 packets) counts its "first packet of a new key", publishes
-// the count, and looks back over the earlier chunks' published counts until
-// it meets an inclusive prefix; its first packets then get port = NEXT_PORT +
-// ordinal (ordinal = prefix + rank in the chunk).  Chunks are numbered by an
-// atomic ticket taken when the workgroup starts, so every chunk a workgroup
-// waits for belongs to a workgroup that is already running: no deadlock.
+// ---- the tail kernel: order the new keys, rewrite the deferred frames ------
+// One small persistent grid whose workgroups take 256-packet chunk tickets.
+// For chunk b a workgroup
+//   1. counts the chunk's first packets of new keys, finds their ordinal
+//      base by a decoupled look-back over the earlier chunks' published
+//      counts (each chunk publishes its count, then looks back until it meets
+//      an inclusive prefix), and assigns port = NEXT_PORT + ordinal: the
+//      slot's port word (released), ADDR_MAP, the commit of the key;
+//   2. rewrites the chunk's deferred frames (a quad per frame), taking each
+//      frame's port from its key's slot -- assigned by this chunk or an
+//      earlier one, so a frame may wait for an earlier chunk's step 1.
+// Every wait is for a lower-numbered chunk, which a running workgroup took
+// (tickets are taken in order by running workgroups), so every wait ends.
+// The workgroup that completes the last chunk advances NEXT_PORT (after
+// every chunk has read it) and clears the next call's counters.
 // Look-back words: epoch << 34 | status << 32 | count (status 1 aggregate,
 // 2 inclusive; a word from an earlier call has another epoch = not yet).
-// NEXT_PORT itself is advanced by K5, after every assignment has read it.
 constexpr uint64_t kLbAgg = 1ull << 32, kLbIncl = 2ull << 32;
 
-__global__ __launch_bounds__(kBlock) void nat64_order(Nat64Args a, uint32_t nb) {
-  __shared__ uint32_t s_chunk, s_prefix;
-  __shared__ uint32_t wcount[kBlock / 64];
-  if (a.pm.state[4u + a.par] == 0u) return;  // nothing deferred: no new key
-  if (threadIdx.x == 0) s_chunk = atomicAdd(&a.pm.state[6u + a.par], 1u);
-  __syncthreads();
-  const uint32_t b = s_chunk;
-  const uint32_t i = b * kBlock + threadIdx.x;
-  const bool f = i < a.n && is_first_new(a, i);
-  const uint64_t mask = __ballot(f);
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  const uint32_t below = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-  if (lane == 0) wcount[wave] = (uint32_t)__popcll(mask);
-  const uint32_t c = (uint32_t)__syncthreads_count(f);
-  if (threadIdx.x == 0) {
-    const uint64_t ep = (uint64_t)(a.epoch & 0x3fffffffu) << 34;
-    uint32_t prefix = 0;
-    if (b == 0) {
-      __hip_atomic_store(&a.lookback[0], ep | kLbIncl | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(&a.lookback[b], ep | kLbAgg | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (uint32_t j = b - 1;; --j) {
-        uint64_t v;
-        do {
-          v = __hip_atomic_load(&a.lookback[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } while ((v & ~0x3ffffffffull) != ep || (v & (3ull << 32)) == 0ull);
-        prefix += (uint32_t)v;
-        if (v & kLbIncl) break;
-      }
-      __hip_atomic_store(&a.lookback[b], ep | kLbIncl | (prefix + c), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_prefix = prefix;
-    if (b == nb - 1u) a.pm.state[8] = prefix + c;  // the batch's new keys, for K5
-  }
-  __syncthreads();
-  uint32_t pre = s_prefix;
-  for (uint32_t w = 0; w < wave; ++w) pre += wcount[w];
-  if (f) {
-    const uint32_t ps = a.pkt_slot[i], slot = ps & kSlotMask;
-    const uint32_t ordinal = pre + below;
-    const uint32_t port = (a.pm.state[0] + ordinal) & 0xffffu;  // NEXT_PORT.fetch_add order
-    a.pm.slots[slot].w[6] = port;
-    a.pkt_slot[i] = ps | kFirstBit;
-    // ADDR_MAP.insert_new(port, key) (main.rs:50): the first mapping of a
-    // port wins, also after NEXT_PORT wraps; ordinals are global
-    const uint64_t tag = ((uint64_t)(a.pm.state[1] + ordinal) << 32) | slot;
-    atomicMin((unsigned long long *)&a.pm.rev[port], (unsigned long long)tag);
-  }
+__device__ __forceinline__ void reset_next_call(const Nat64Args &a) {
+  a.pm.state[4u + (a.par ^ 1u)] = 0u;  // deferred-list counter
+  a.pm.state[6u + (a.par ^ 1u)] = 0u;  // chunk ticket
+  a.pm.state[9u + (a.par ^ 1u)] = 0u;  // chunks done
 }
 
-// ---- K5: the deferred frames (phase 2's rewrite, list-driven) + commit -------
-__global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_deferred(Nat64Args a) {
-  const uint32_t cnt = a.pm.state[4u + a.par];
-  if (cnt != 0u && blockIdx.x == 0 && threadIdx.x == 0) {  // advance NEXT_PORT (AtomicU16 wrap)
-    const uint32_t total = a.pm.state[8];
-    a.pm.state[0] = (a.pm.state[0] + total) & 0xffffu;
-    a.pm.state[1] += total;
+__global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_tail(Nat64Args a, uint32_t nb) {
+  __shared__ uint32_t s_chunk, s_prefix;
+  __shared__ uint32_t wcount[kBlock / 64];
+  __shared__ uint32_t s_def[kBlock];
+  if (a.pm.state[4u + a.par] == 0u) {  // nothing deferred: no new key
+    if (blockIdx.x == 0 && threadIdx.x == 0) reset_next_call(a);
+    return;
   }
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t g = threadIdx.x % kFG;
   const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
   const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
-  for (uint32_t e = blockIdx.x * (kBlock / kFG) + threadIdx.x / kFG; e < cnt;
-       e += gridDim.x * (kBlock / kFG)) {
-    const uint32_t p = a.defer[e];
-    const uint32_t ps = a.pkt_slot[p], slot = ps & kSlotMask;
-    const u32x4 hv = a.rec_h[p];
-    const uint2 bv = a.rec_b[p];
-    FrameRec f;
-    f.in_off = a.off[p];
-    f.o_off = a.out_off[p];
-    f.new_len = (uint32_t)a.len[p] - 20u;
-    f.info = (bv.y & 3u) | (a.pm.slots[slot].w[6] << 16);  // port from K4
-    f.V[0] = hv[0]; f.V[1] = hv[1]; f.V[2] = hv[2]; f.V[3] = hv[3]; f.V[4] = bv.x;
-#pragma unroll
-    for (int j = 5; j < 10; ++j) f.V[j] = 0u;
-    f.ph = 0u;
-    rewrite_dispatch<true>(a, rs, ors, g, f, true);
-    if (g == 0u) {
-      a.out_len[p] = (uint16_t)f.new_len;
-      if (ps & kFirstBit) {  // commit the new key (PORT_MAP.insert_new, main.rs:49)
+  bool more = true;
+  while (more) {
+    if (threadIdx.x == 0) s_chunk = atomicAdd(&a.pm.state[6u + a.par], 1u);
+    __syncthreads();
+    const uint32_t b = s_chunk;
+    more = b < nb;  // workgroup-uniform
+    if (more) {
+      // 1. order
+      const uint32_t i = b * kBlock + threadIdx.x;
+      const bool f = i < a.n && is_first_new(a, i);
+      const uint64_t mask = __ballot(f);
+      const uint32_t below = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+      if (lane == 0) wcount[wave] = (uint32_t)__popcll(mask);
+      const uint32_t c = (uint32_t)__syncthreads_count(f);
+      if (threadIdx.x == 0) {
+        const uint64_t ep = (uint64_t)(a.epoch & 0x3fffffffu) << 34;
+        uint32_t prefix = 0;
+        if (b == 0) {
+          __hip_atomic_store(&a.lookback[0], ep | kLbIncl | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          __hip_atomic_store(&a.lookback[b], ep | kLbAgg | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (uint32_t j = b - 1;; --j) {
+            uint64_t v;
+            do {
+              v = __hip_atomic_load(&a.lookback[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } while ((v & ~0x3ffffffffull) != ep || (v & (3ull << 32)) == 0ull);
+            prefix += (uint32_t)v;
+            if (v & kLbIncl) break;
+          }
+          __hip_atomic_store(&a.lookback[b], ep | kLbIncl | (prefix + c), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_prefix = prefix;
+        if (b == nb - 1u) a.pm.state[8] = prefix + c;  // the batch's new keys
+      }
+      __syncthreads();
+      uint32_t pre = s_prefix;
+      for (uint32_t w = 0; w < wave; ++w) pre += wcount[w];
+      uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
+      if (f) {
+        const uint32_t slot = ps & kSlotMask;
+        const uint32_t ordinal = pre + below;
+        const uint32_t port = (a.pm.state[0] + ordinal) & 0xffffu;  // NEXT_PORT.fetch_add order
+        // ADDR_MAP.insert_new(port, key) (main.rs:50): the first mapping of a
+        // port wins, also after NEXT_PORT wraps; ordinals are global
+        const uint64_t tag = ((uint64_t)(a.pm.state[1] + ordinal) << 32) | slot;
+        atomicMin((unsigned long long *)&a.pm.rev[port], (unsigned long long)tag);
+        // PORT_MAP.insert_new (main.rs:49): commit the key for later batches
         a.pm.slots[slot].w[7] = 0xffffffffu;
         a.pm.slots[slot].w[0] = kPersist;
+        __hip_atomic_store(&a.pm.slots[slot].w[6], port, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // 2. the chunk's deferred frames: compact them, a quad per frame
+      const bool d = ps != kNoSlot;
+      const uint64_t dm = __ballot(d);
+      const uint32_t dbelow = (uint32_t)__popcll(dm & ((1ull << lane) - 1ull));
+      __syncthreads();  // wcount reused
+      if (lane == 0) wcount[wave] = (uint32_t)__popcll(dm);
+      const uint32_t nd = (uint32_t)__syncthreads_count(d);
+      uint32_t dpre = 0;
+      for (uint32_t w = 0; w < wave; ++w) dpre += wcount[w];
+      if (d) s_def[dpre + dbelow] = i;
+      __syncthreads();
+      for (uint32_t e = threadIdx.x / kFG; e < nd; e += kBlock / kFG) {
+        const uint32_t p = s_def[e];
+        const uint32_t slot = a.pkt_slot[p] & kSlotMask;
+        uint32_t port;
+        while ((port = __hip_atomic_load(&a.pm.slots[slot].w[6], __ATOMIC_ACQUIRE,
+                                         __HIP_MEMORY_SCOPE_AGENT)) == kNoPort)
+          __builtin_amdgcn_s_sleep(1);
+        const u32x4 hv = a.rec_h[p];
+        const uint2 bv = a.rec_b[p];
+        FrameRec fr;
+        fr.in_off = a.off[p];
+        fr.o_off = a.out_off[p];
+        fr.new_len = (uint32_t)a.len[p] - 20u;
+        fr.info = (bv.y & 3u) | (port << 16);
+        fr.V[0] = hv[0]; fr.V[1] = hv[1]; fr.V[2] = hv[2]; fr.V[3] = hv[3]; fr.V[4] = bv.x;
+#pragma unroll
+        for (int j = 5; j < 10; ++j) fr.V[j] = 0u;
+        fr.ph = 0u;
+        rewrite_dispatch<true>(a, rs, ors, g, fr, true);
+        if (g == 0u) a.out_len[p] = (uint16_t)fr.new_len;
+      }
+      // 3. done with chunk b: the last one advances NEXT_PORT
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(&a.pm.state[9u + a.par], 1u, __ATOMIC_ACQ_REL,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        if (old == nb - 1u) {  // every chunk has read NEXT_PORT: advance it (AtomicU16 wrap)
+          const uint32_t total = a.pm.state[8];
+          a.pm.state[0] = (a.pm.state[0] + total) & 0xffffu;
+          a.pm.state[1] += total;
+          reset_next_call(a);
+        }
       }
     }
-  }
-  // the other parity's list counter is the next call's: clear it for that call
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    a.pm.state[4u + (a.par ^ 1u)] = 0u;  // deferred-list counter
-    a.pm.state[6u + (a.par ^ 1u)] = 0u;  // chunk ticket
+    __syncthreads();  // s_chunk, s_prefix, wcount, s_def are rewritten next round
   }
 }
 
@@ -997,12 +1311,19 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
     pm.state[6] = 0u;  // look-back chunk tickets, by call parity
     pm.state[7] = 0u;
     pm.state[8] = 0u;  // new keys of the last batch
+    pm.state[9] = 0u;  // chunks ordered, by call parity
+    pm.state[10] = 0u;
   }
 }
 
 }  // namespace
 
 uint32_t nat64_num_blocks(uint32_t n) { return (n + kBlock - 1) / kBlock; }
+
+#ifndef CGPU_NAT64_TAIL_GRID
+#define CGPU_NAT64_TAIL_GRID 256
+#endif
+constexpr uint32_t kTailGrid = CGPU_NAT64_TAIL_GRID;  // workgroups of K2 / K5
 
 hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStream_t s) {
   const uint32_t cap = pm.cap_mask + 1u > 65536u ? pm.cap_mask + 1u : 65536u;
@@ -1013,10 +1334,12 @@ hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStr
 hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const uint32_t nb = nat64_num_blocks(a.n);
-  const uint32_t nbq = (a.n + kBlock / kFG - 1) / (kBlock / kFG);  // one quad per frame
-  hipLaunchKernelGGL(nat64_6to4_fused, dim3(nbq), dim3(kBlock), 0, s, a);
-  hipLaunchKernelGGL(nat64_order, dim3(nb), dim3(kBlock), 0, s, a, nb);
-  hipLaunchKernelGGL(nat64_6to4_deferred, dim3(nbq < 2048u ? nbq : 2048u), dim3(kBlock), 0, s, a);
+  const uint32_t fpb = (kBlock / 64u) * kRowFrames;  // fused: kRowFrames frames per wave
+  const uint32_t nbf = (a.n + fpb - 1) / fpb;
+  hipLaunchKernelGGL(nat64_6to4_fused, dim3(nbf), dim3(kBlock), 0, s, a);
+  // the tail (order + deferred rewrite) is one small persistent grid; in the
+  // steady state (no new key) it returns at once
+  hipLaunchKernelGGL(nat64_tail, dim3(kTailGrid), dim3(kBlock), 0, s, a, nb);
   return hipGetLastError();
 }
 

@@ -96,15 +96,17 @@ def test_bench_nat64_config_every_byte(ctx):
     a, o, l = w["arena"], w["off"], w["len"]
     gw = packets.Nat64Gateway(ctx, capacity_log2=17)
     pm = oracle_lib.PortMap()
+    oo, size = w["out_off"], w["out_size"]  # the bench's packed egress layout
     for p in range(2):
-        g = _gpu_nat(gw, "6to4", a, o, l, o, len(a))
-        ref = pm.nat_6to4(a, o, l)
+        g = _gpu_nat(gw, "6to4", a, o, l, oo, size)
+        ref = pm.nat_6to4(a, o, l, oo, size)
         _compare_nat(g, ref, f"6to4 pass {p}")
         assert (ref[2] == N.ACT).all()
         assert gw.next_port() == pm.next_port() and gw.size() == pm.size()
-    ra, ro, rl = synth.nat64_replies(ref[0], o, ref[1])
-    g = _gpu_nat(gw, "4to6", ra, ro, rl, ro, len(ra))
-    _compare_nat(g, pm.nat_4to6(ra, ro, rl, ro, len(ra)), "4to6")
+    ra, ro, rl = synth.nat64_replies(ref[0], oo, ref[1])
+    o6 = (np.arange(len(ro), dtype=np.int64) * 256).astype(np.uint32)  # +20 B per frame
+    g = _gpu_nat(gw, "4to6", ra, ro, rl, o6, 256 * len(ro) + 64)
+    _compare_nat(g, pm.nat_4to6(ra, ro, rl, o6, 256 * len(ro) + 64), "4to6")
     assert (g[2] == N.ACT).all()
     gw.close()
 

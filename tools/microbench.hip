@@ -175,6 +175,28 @@ __global__ __launch_bounds__(256) void copy_shift(const uint8_t *in, uint8_t *ou
   }
 }
 
+// the nat64 6to4 shape in rows of 16 lanes (the rows path of nat64.hip):
+// aligned 16-B loads, output chunk l >= 2 = {in(l+1).yzw, in(l+2).x} by DPP
+// row shifts, 236-B output, last chunk b96
+template <int CTRL>
+__device__ __forceinline__ uint32_t dppz_mb(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, true);
+}
+template <uint32_t OSTRIDE>
+__global__ __launch_bounds__(256) void copy_rows_dpp(const uint8_t *in, uint8_t *out, uint32_t n) {
+  const uint32_t l = threadIdx.x & 15u, p = blockIdx.x * 16u + threadIdx.x / 16u;
+  auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(in), (short)0, (int)(n * 256u), 0x00020000);
+  auto os = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(n * 256u), 0x00020000);
+  const u32x4 A = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(p < n ? p * 256u + 16u * l : 0xffffff00u), 0, 0);
+  u32x4 o = {dppz_mb<0x101>(A[1]), dppz_mb<0x101>(A[2]), dppz_mb<0x101>(A[3]), dppz_mb<0x102>(A[0])};
+  if (l < 2u) o = A;
+  if (p >= n) return;
+  if (16u * l + 16u <= 236u)
+    __builtin_amdgcn_raw_buffer_store_b128(o, os, (int)(p * OSTRIDE + 16u * l), 0, 0);
+  else if (16u * l < 236u)
+    __builtin_amdgcn_raw_buffer_store_b96(__builtin_shufflevector(o, o, 0, 1, 2), os, (int)(p * OSTRIDE + 16u * l), 0, 0);
+}
+
 // copy mapping sweep: G lanes per 256-B frame, 16/G chunks per lane, chunk
 // order contiguous per lane (IL=false) or interleaved across the group (IL=true),
 // cache policy AUX on loads and stores.
@@ -351,18 +373,22 @@ int main(int argc, char **argv) {
   }
   {  // nat64-shaped copies over 1M x 256-B frames (separate, larger arena)
     const uint32_t nf = n;
-    uint8_t *fin[4], *fout;
+    uint8_t *fin[4], *fouts[4];
     for (int r = 0; r < 4; ++r) CK(hipMalloc(&fin[r], (size_t)nf * 256));
-    CK(hipMalloc(&fout, (size_t)nf * 256));
+    for (int r = 0; r < 4; ++r) CK(hipMalloc(&fouts[r], (size_t)nf * 256));
+    // outputs rotate like the inputs (one fixed 256 MiB output would stay in
+    // the Infinity Cache and absorb the writes)
+    uint8_t *fout = fouts[0];
+    (void)fout;
     for (int r = 0; r < 4; ++r) CK(hipMemset(fin[r], r, (size_t)nf * 256));
     const double fb = (double)nf * (256 + 240);
     time_it("copy_frames_shift20_240B", fb, [&](int r) {
-      hipLaunchKernelGGL(copy_frames<20>, dim3((nf + 63) / 64), dim3(256), 0, st, fin[r % 4], fout, nf, 240u);
+      hipLaunchKernelGGL(copy_frames<20>, dim3((nf + 63) / 64), dim3(256), 0, st, fin[r % 4], fouts[r % 4], nf, 240u);
     });
 #define MAPCASE(G, IL, AUX)                                                                 \
   time_it("copy_map_G" #G "_IL" #IL "_aux" #AUX, (double)nf * 512, [&](int r) {               \
     hipLaunchKernelGGL((copy_map<G, IL, AUX>), dim3((nf * G + 255) / 256), dim3(256), 0, st,  \
-                       fin[r % 4], fout, nf);                                                 \
+                       fin[r % 4], fouts[r % 4], nf);                                                 \
   });
     MAPCASE(1, false, 0) MAPCASE(2, false, 0) MAPCASE(4, false, 0) MAPCASE(4, true, 0)
     MAPCASE(8, true, 0) MAPCASE(16, true, 0) MAPCASE(16, true, 2) MAPCASE(4, true, 2)
@@ -370,11 +396,17 @@ int main(int argc, char **argv) {
 #define SHIFTCASE(G, AUX)                                                                   \
   time_it("copy_shift20_G" #G "_aux" #AUX, (double)nf * (256 + 236), [&](int r) {             \
     hipLaunchKernelGGL((copy_shift<G, AUX>), dim3((nf * G + 255) / 256), dim3(256), 0, st,    \
-                       fin[r % 4], fout, nf);                                               \
+                       fin[r % 4], fouts[r % 4], nf);                                               \
   });
     SHIFTCASE(4, 0) SHIFTCASE(8, 0) SHIFTCASE(16, 0) SHIFTCASE(16, 2) SHIFTCASE(4, 2)
+    time_it("copy_rows_dpp_236B_slots256", (double)nf * (256 + 236), [&](int r) {
+      hipLaunchKernelGGL(copy_rows_dpp<256>, dim3((nf + 15) / 16), dim3(256), 0, st, fin[r % 4], fouts[r % 4], nf);
+    });
+    time_it("copy_rows_dpp_236B_packed", (double)nf * (256 + 236), [&](int r) {
+      hipLaunchKernelGGL(copy_rows_dpp<236>, dim3((nf + 15) / 16), dim3(256), 0, st, fin[r % 4], fouts[r % 4], nf);
+    });
     time_it("copy_frames_shift0_256B", (double)nf * 512, [&](int r) {
-      hipLaunchKernelGGL(copy_frames<0>, dim3((nf + 63) / 64), dim3(256), 0, st, fin[r % 4], fout, nf, 256u);
+      hipLaunchKernelGGL(copy_frames<0>, dim3((nf + 63) / 64), dim3(256), 0, st, fin[r % 4], fouts[r % 4], nf, 256u);
     });
   }
   cgpu_ctx_destroy(ctx);
