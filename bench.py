@@ -259,7 +259,7 @@ METRIC = "Mpps device-resident parse+cksum+hash @64/256/1500B; % HBM-read roofli
 SIZES = ("parse256", "parse1500", "imix", "imix_csum", "nat64")
 # BASELINE config 5: IMIX shards, one per GPU (the `shards` object)
 SHARD_CONFIG = "imix"
-MIN_WARM_S = 0.06  # device time of warm-up before any timed region (steady clocks)
+MIN_WARM_S = 0.15  # device time of warm-up before any timed region (steady clocks)
 PORTMAP_LOG2 = int(os.environ.get("CGPU_BENCH_PORTMAP_LOG2", "20"))  # Nat64Gateway default
 
 
@@ -323,17 +323,31 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None):
                                            direction) for k in range(2 * copies)]
     cycle = len(launchers)
 
-    # warm-up: >= `warmup` launches and >= MIN_WARM_S of device time
+    # warm-up: >= `warmup` launches and >= MIN_WARM_S of device time, issued
+    # back to back (no host sync in between) so the clocks are at their
+    # steady state when the timed region starts
     k = 0
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    while k < warmup or time.perf_counter() - t0 < MIN_WARM_S:
-        for _ in range(16):
-            launchers[k % cycle]()
-            k += 1
-        torch.cuda.synchronize(dev)
+    for _ in range(32):
+        launchers[k % cycle]()
+        k += 1
+    torch.cuda.synchronize(dev)
+    per = (time.perf_counter() - t0) / 32
+    for _ in range(max(warmup, int(MIN_WARM_S / per) + 1)):
+        launchers[k % cycle]()
+        k += 1
+    torch.cuda.synchronize(dev)
 
+    # HIP events on the launch stream bracket the K timed launches (ev0 just
+    # before the first, ev1 behind the last): (ev1 - ev0) / K is the per-launch
+    # device time (kernel plus the back-to-back dispatch gap).  Both are
+    # recorded once here first: torch creates an event's HIP object at its
+    # first record, which must not happen inside the timed region.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
     state = {"k": k, "left": steps}
 
     def one():
