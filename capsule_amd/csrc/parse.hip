@@ -50,6 +50,13 @@ constexpr uint32_t kSlotPieces = 2;  // longest tail (256-B pieces) summed in sl
 #define CGPU_SLOT_IT 4
 #endif
 constexpr uint32_t kSlotIt = CGPU_SLOT_IT;  // slots per 16-lane row and round (loads in flight)
+#ifndef CGPU_PARSE_ROWS
+#define CGPU_PARSE_ROWS 1
+#endif
+#ifndef CGPU_PARSE_ROW_MAX
+#define CGPU_PARSE_ROW_MAX 512
+#endif
+constexpr uint32_t kRowMaxLen = CGPU_PARSE_ROW_MAX;  // the rows path: frames up to 2 pieces
 
 __device__ __forceinline__ uint32_t sel3(uint32_t k, uint32_t a, uint32_t b, uint32_t c) {
   return k == 0u ? a : (k == 1u ? b : c);
@@ -115,7 +122,87 @@ __device__ __forceinline__ uint32_t chunk_excess(u32x4 v, uint32_t c, uint32_t f
   return e;
 }
 
-template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT>
+// ---- the rows path (L4 checksum configs, waves of long frames) -----------
+// A wave whose frames are 16-B aligned, at most 512 B long and mostly
+// (>= half) at least 128 B long reads each frame once, in rows: 16 lanes
+// take one 256-B piece of one frame per load instruction (four whole frames
+// per instruction, full lines), sum its u16 words (the frame's last chunk
+// masked at its end) and reduce them over the row with DPP; the first 96 B
+// of every frame pass through wave-private LDS to the frame's own lane.  The
+// lane then has its window P and the exact word sum of the whole frame;
+// the checksum span's sum is that sum minus the words before the span.  No
+// line is fetched twice, as the per-lane window + tail passes do for line 0
+// of long frames (window: bytes 0..63; tail: bytes 64..127, later).
+// Frames are processed in two halves of 32 (LDS: 32 x 96 B + sums per wave).
+constexpr uint32_t kRowHalf = 32;
+constexpr uint32_t kRowLds = kRowHalf * kWin + kRowHalf;  // dwords per wave
+
+__device__ __forceinline__ void rows_prologue(rsrc_t rs, uint32_t off, uint32_t len, uint32_t lane,
+                                              uint32_t *L, uint32_t (&P)[kWin], uint32_t &s_all) {
+  const uint32_t row = lane >> 4, l = lane & 15u;
+  uint32_t npass = 0;  // 256-B pieces of the wave's longest frame
+#pragma unroll
+  for (uint32_t p = 0; p < kRowMaxLen / 256u; ++p)
+    if (__ballot(len > 256u * p)) npass = p + 1u;
+  uint32_t *sums = L + kRowHalf * kWin;
+#pragma unroll
+  for (uint32_t half = 0; half < 2u; ++half) {
+    for (uint32_t p = 0; p < npass; ++p) {
+      // the half's 8 rounds in two groups of 4 loads in flight (the kernel
+      // runs at 8 waves per SIMD: 64 VGPRs)
+#pragma unroll
+      for (uint32_t rg = 0; rg < kRowHalf / 16u; ++rg) {
+        u32x4 v[4];
+        uint32_t fl[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4u; ++u) {
+          const uint32_t f = kRowHalf * half + 16u * rg + 4u * u + row;
+          const uint32_t fo = __shfl(off, (int)f);
+          fl[u] = __shfl(len, (int)f);
+          const uint32_t c = 16u * p + l;
+          v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * c < fl[u] ? fo + 16u * c : kNoRead), 0, 0);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 4u; ++u) {
+          const uint32_t fr = 16u * rg + 4u * u + row;  // frame within the half
+          if (p == 0u && l < 6u) *reinterpret_cast<u32x4 *>(L + fr * kWin + 4u * l) = v[u];
+          const uint32_t b0 = 256u * p + 16u * l;
+          const uint32_t rem = fl[u] > b0 ? fl[u] - b0 : 0u;
+          u32x4 x4 = v[u];
+          if (__ballot(rem < 16u)) {
+#pragma unroll
+            for (uint32_t t = 0; t < 4u; ++t) {
+              const uint32_t lo = 4u * t;
+              x4[t] &= rem >= lo + 4u ? 0xffffffffu : (rem <= lo ? 0u : 0xffffffffu >> (8u * (lo + 4u - rem)));
+            }
+          }
+          uint32_t x = sum4(x4, 0u);
+          x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+          x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+          x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+          x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+          if (l == 15u) sums[fr] = p == 0u ? x : sums[fr] + x;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if ((lane >> 5) == half) {
+      const uint32_t fr = lane & (kRowHalf - 1u);
+#pragma unroll
+      for (int m = 0; m < kWin / 4; ++m) {
+        const u32x4 t = *reinterpret_cast<const u32x4 *>(L + fr * kWin + 4u * m);
+        P[4 * m] = t[0];
+        P[4 * m + 1] = t[1];
+        P[4 * m + 2] = t[2];
+        P[4 * m + 3] = t[3];
+      }
+      s_all = npass ? sums[fr] : 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+}
+
+template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT, bool ROWS>
 __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   // No early exit: lanes past n run with len 0 (status BadOffset) and store
@@ -132,8 +219,24 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   // --- the packet-relative window P ---------------------------------------
   uint32_t P[kWin];
   uint32_t wlim = 96u;  // packet bytes the window holds
+  bool rows = false;     // the rows path (above): window and frame sum from rows
+  uint32_t s_all = 0;
+#if CGPU_PARSE_ROWS
+  if (ROWS) {
+    const bool bad = valid && ((off & 15u) != 0u || len > kRowMaxLen ||
+                               (uint64_t)off + len + 16u > (uint64_t)a.arena_len);
+    const uint64_t vm = __ballot(valid);
+    rows = vm && !__ballot(bad) &&
+           2u * (uint32_t)__popcll(__ballot(valid && len >= 128u)) >= (uint32_t)__popcll(vm);
+  }
+#endif
   const bool slow = (off & 3u) != 0u || (uint64_t)off + 96u > (uint64_t)a.arena_len;
-  if (__ballot(slow)) {
+  if (ROWS && rows) {
+#if CGPU_PARSE_ROWS
+    __shared__ uint32_t rlds[kBlock / 64][kRowLds];
+    rows_prologue(rs, valid ? off : 0u, valid ? len : 0u, threadIdx.x & 63u, rlds[threadIdx.x >> 6], P, s_all);
+#endif
+  } else if (__ballot(slow)) {
     load_window_general(rs, a.arena_len, off, len, P);
   } else {
 #pragma unroll
@@ -318,7 +421,24 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   }
   uint32_t s = 0, stored_le = 0, t_b = 0;
   bool has_tail = false;
-  if (L4C && l4_ok) {
+  if (ROWS && L4C && l4_ok && rows) {
+    // the rows path: the same byte range's sum is the frame's word sum
+    // minus the words before it (start = 22 or 26, + 4 per VLAN tag; even)
+    const uint32_t start = (v6 ? 22u : 26u) + 4u * k;
+    uint32_t pre = 0;
+#pragma unroll
+    for (int j = 0; j < 11; ++j) {
+      const uint32_t lo = 4u * (uint32_t)j;
+      pre = sad16(lo + 4u <= start ? P[j] : (lo < start ? (P[j] & 0xffffu) : 0u), pre);
+    }
+    s = s_all - pre;
+    stored_le = udp    ? (v6 ? (Q[15] & 0xffffu) : (Q[10] & 0xffffu))
+                : icmp ? (v6 ? (Q[14] & 0xffffu) : (Q[9] & 0xffffu))
+                       : (v6 ? (Q[17] >> 16) : (Q[12] >> 16));
+    s -= stored_le;
+    if (icmp && !v6) s -= (Q[6] >> 16) + (Q[7] & 0xffffu) + (Q[7] >> 16) + (Q[8] & 0xffffu);
+  }
+  if (L4C && l4_ok && (!(ROWS && rows) || xok)) {
     // pseudo-header addresses + span [l4, len) (udp.rs:204-219, tcp.rs:
     // 462-477, checksum.rs:56-128) are one contiguous byte range: [26, len)
     // for v4, [22, len) for v6; the stored checksum field is subtracted.
@@ -630,7 +750,14 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
 template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT>
 hipError_t launch_t(const ParseArgs &a, hipStream_t s) {
   const uint32_t grid = (a.n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT>), dim3(grid), dim3(kBlock), 0, s, a);
+  // The rows path is compiled into a variant that the checksum configs get
+  // when the batch's mean slot (arena bytes per packet) is 128..640 B: long
+  // frames, but not jumbo ones; each wave still decides by its own frames.
+  const uint64_t mean = (uint64_t)a.arena_len / a.n;
+  if (L4C && CGPU_PARSE_ROWS && mean >= 128u && mean <= 640u)
+    hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, true>), dim3(grid), dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, false>), dim3(grid), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 

@@ -287,3 +287,33 @@ def test_reference_fixtures_with_extensions(ctx):
     for acc in (N.F_ACCEPT_ALL, N.F_ACCEPT_V6 | N.F_ACCEPT_TCP, N.F_ACCEPT_V6 | N.F_ACCEPT_UDP):
         for feat in (0, N.F_CSUM_L4, N.F_FLOW_HASH, 0x70, 0x70 | N.F_ACCEPT_ICMP):
             assert_ext_parity(ctx, arena, off, ln, acc | feat | N.F_V6_EXT)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_rows_path_long_frames(ctx, seed):
+    """Batches whose mean slot is 128..640 B run the rows variant; its waves
+    of aligned frames up to 512 B (at least half of them >= 128 B) read every
+    frame in rows and take the checksum span as the frame's word sum minus
+    the words before the span.  Every kind, VLAN depth, length 42..512
+    (short frames mixed in), corrupted bytes, ICMP, wrong types: bit-exact."""
+    rng = np.random.default_rng(seed)
+    kinds = [synth.V4_UDP, synth.V4_TCP, synth.V6_UDP, synth.V6_TCP, synth.V4_ICMP,
+             synth.V6_ICMP]
+    frames = []
+    for j in range(6000):
+        kind = kinds[int(rng.integers(0, len(kinds)))]
+        vlan = int(rng.integers(0, 3))
+        need = 14 + 4 * vlan + (20 if kind[0] == 4 else 40) + synth.l4_header_len(kind[1])
+        L = int(rng.integers(need, 513)) if rng.random() < 0.75 else int(rng.integers(need, 128))
+        fr = synth.build_frames(rng, 1, kind, max(L, need), vlan)[0]
+        r = rng.random()
+        if r < 0.05:
+            fr[int(rng.integers(0, len(fr)))] ^= 0x41
+        elif r < 0.08:
+            fr = fr[: int(rng.integers(0, len(fr) + 1))]
+        frames.append(bytes(fr))
+    for slot in (256, 512):
+        arena, off, ln = synth.pack_frames(frames, slot)
+        for flags in (ALL, ALL | N.F_ACCEPT_ICMP, N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | N.F_CSUM_L4):
+            om = assert_parity(ctx, arena, off, ln, flags, fields=True)
+        assert (om & N.META_L4_CSUM_OK).sum() > 3000
