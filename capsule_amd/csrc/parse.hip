@@ -97,6 +97,20 @@ __device__ __forceinline__ uint32_t sum_to_end(const uint32_t (&Q)[kWin - 2], ui
   return acc;
 }
 
+// The same for a wave-uniform wend (an SGPR): whole words are summed without
+// a mask, and the words past the end are skipped by scalar branches.
+template <int J0>
+__device__ __forceinline__ uint32_t sum_to_end_s(const uint32_t (&Q)[kWin - 2], uint32_t wend,
+                                                 uint32_t acc) {
+#pragma unroll
+  for (int j = J0; j < (int)(kQEnd / 4); ++j) {
+    const uint32_t lo = 4u * (uint32_t)j;
+    if (wend <= lo) break;
+    acc = sad16(wend < lo + 4u ? Q[j] & (0xffffffffu >> (8u * (lo + 4u - wend))) : Q[j], acc);
+  }
+  return acc;
+}
+
 // Tail sums.  A 1 KiB piece [b, b + 1024) of a tail [from, to) (absolute
 // arena offsets, b = from & ~15 + 1024 j) is loaded by the whole wave, 16 B
 // per lane; a lane loads its chunk only if the chunk overlaps [from, to), and
@@ -202,7 +216,11 @@ __device__ __forceinline__ void rows_prologue(rsrc_t rs, uint32_t off, uint32_t 
   }
 }
 
-template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT, bool ROWS>
+// V4U: the accept set has no IPv6, TCP, ICMP or extension bit (the typed
+// parse::<Ipv4>() -> parse::<Udp<Ipv4>>() chain of the reference bench,
+// bench/packets.rs:65-69): every IPv6 / TCP / ICMP branch is compiled out,
+// as Rust monomorphises the typed chain.
+template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT, bool V4U, bool ROWS>
 __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   // No early exit: lanes past n run with len 0 (status BadOffset) and store
@@ -259,8 +277,8 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       const uint32_t kk = mk == 0x8100u ? 1u : (mk == 0x88a8u ? 2u : 0u);
       const uint32_t et = be16_lo(sel3(kk, P[3], P[4], P[5]));
       const uint32_t w5 = sel3(kk, P[5], P[6], P[7]);  // normalized bytes 20..23
-      const bool is6 = et == 0x86ddu;
-      const uint32_t pr = is6 ? (w5 & 0xffu) : (w5 >> 24);
+      const bool is6 = !V4U && et == 0x86ddu;
+      const uint32_t pr = V4U ? 17u : (is6 ? (w5 & 0xffu) : (w5 >> 24));
       const uint32_t hdr_end = (is6 ? 54u + 4u * kk : 0u) + (pr == 6u ? 20u : 8u);
 #pragma unroll
       for (int c = 4; c < 6; ++c) {
@@ -301,7 +319,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
 
   // --- status: the first failing step of the reference chain --------------
   const bool v4 = ether_type == 0x0800u && (a.accept & CGPU_F_ACCEPT_V4);
-  const bool v6 = ether_type == 0x86ddu && (a.accept & CGPU_F_ACCEPT_V6);
+  const bool v6 = !V4U && ether_type == 0x86ddu && (a.accept & CGPU_F_ACCEPT_V6);
   const uint32_t l3_len = v6 ? 40u : 20u;
   const uint32_t proto0 = v6 ? (Q[5] & 0xffu) : (Q[5] >> 24);
   // --- IPv6 extension header (CGPU_F_V6_EXT): SegmentRouting (43) or
@@ -352,9 +370,9 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     }
   }
   const bool udp = proto == 17u && (a.accept & CGPU_F_ACCEPT_UDP);
-  const bool tcp = proto == 6u && (a.accept & CGPU_F_ACCEPT_TCP);
+  const bool tcp = !V4U && proto == 6u && (a.accept & CGPU_F_ACCEPT_TCP);
   // ProtocolNumbers::Icmpv4 (1) under IPv4, Icmpv6 (58) under IPv6 (ip/mod.rs:41-75)
-  const bool icmp = proto == (v6 ? 58u : 1u) && (a.accept & CGPU_F_ACCEPT_ICMP);
+  const bool icmp = !V4U && proto == (v6 ? 58u : 1u) && (a.accept & CGPU_F_ACCEPT_ICMP);
   const uint32_t l4_len = udp ? 8u : (icmp ? 4u : 20u);
   uint32_t st = CGPU_PKT_OK;
   bool eth_ok = false, l3_ok = false;
@@ -450,7 +468,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     const uint32_t wq = wlim - 4u * k < kQEnd ? wlim - 4u * k : kQEnd;  // normalized window limit
     const uint32_t wend = endn <= wq ? endn : wq - ((off + wq + 4u * k) & 15u);
     if (!__ballot(wend != __builtin_amdgcn_readfirstlane(wend))) {
-      s = sum_to_end<7>(Q, __builtin_amdgcn_readfirstlane(wend), s);  // scalar masks
+      s = sum_to_end_s<7>(Q, __builtin_amdgcn_readfirstlane(wend), s);  // scalar masks
     } else {
       s = sum_to_end<7>(Q, wend, s);
     }
@@ -747,7 +765,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
 
 }
 
-template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT>
+template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT, bool V4U>
 hipError_t launch_t(const ParseArgs &a, hipStream_t s) {
   const uint32_t grid = (a.n + kBlock - 1) / kBlock;
   // The rows path is compiled into a variant that the checksum configs get
@@ -755,15 +773,19 @@ hipError_t launch_t(const ParseArgs &a, hipStream_t s) {
   // frames, but not jumbo ones; each wave still decides by its own frames.
   const uint64_t mean = (uint64_t)a.arena_len / a.n;
   if (L4C && CGPU_PARSE_ROWS && mean >= 128u && mean <= 640u)
-    hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, V4U, true>), dim3(grid), dim3(kBlock), 0, s, a);
   else
-    hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, false>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, V4U, false>), dim3(grid), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
 template <bool IPC, bool L4C, bool HASH, bool FIELDS>
 hipError_t launch_e(const ParseArgs &a, bool ext, hipStream_t s) {
-  return ext ? launch_t<IPC, L4C, HASH, FIELDS, true>(a, s) : launch_t<IPC, L4C, HASH, FIELDS, false>(a, s);
+  if (ext) return launch_t<IPC, L4C, HASH, FIELDS, true, false>(a, s);
+  // IPv4/UDP only (no header record): the monomorphised variant
+  constexpr uint32_t kNotV4U = CGPU_F_ACCEPT_V6 | CGPU_F_ACCEPT_TCP | CGPU_F_ACCEPT_ICMP;
+  if (!FIELDS && !(a.accept & kNotV4U)) return launch_t<IPC, L4C, HASH, FIELDS, false, !FIELDS>(a, s);
+  return launch_t<IPC, L4C, HASH, FIELDS, false, false>(a, s);
 }
 
 template <bool IPC, bool L4C, bool HASH>

@@ -83,6 +83,9 @@ def test_reference_fixtures_every_flag_combination(ctx):
     for acc in list(range(16)) + [a | N.F_ACCEPT_ICMP for a in range(16)]:
         for feat in (0, N.F_CSUM_IP, N.F_CSUM_L4, N.F_FLOW_HASH, 0x70):
             assert_parity(ctx, arena, off, ln, acc | feat, fields=True)
+            if not acc & (N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | N.F_ACCEPT_ICMP):
+                # no header record: the monomorphised IPv4/UDP variant
+                assert_parity(ctx, arena, off, ln, acc | feat, fields=False)
     assert_parity(ctx, arena, off, ln, ALL, fields=False)
 
 
@@ -94,6 +97,9 @@ def test_fuzz_unaligned_edge_cases(ctx, seed):
                   ALL | N.F_ACCEPT_ICMP, N.F_ACCEPT_ICMP | N.F_CSUM_L4 | N.F_CSUM_IP):
         assert_parity(ctx, arena, off, ln, flags, fields=True)
     assert_parity(ctx, arena, off, ln, ALL, fields=False)
+    v4u = N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP | N.F_CSUM_L4 | N.F_FLOW_HASH
+    assert_parity(ctx, arena, off, ln, v4u, fields=False)  # the IPv4/UDP variant
+    assert_parity(ctx, arena, off, ln, v4u & ~N.F_ACCEPT_UDP, fields=False)
 
 
 def test_every_length_boundary(ctx):
@@ -115,6 +121,8 @@ def test_every_length_boundary(ctx):
         arena = np.concatenate([np.zeros(shift, np.uint8), arena])
         assert_parity(ctx, arena, off + shift, ln, ALL)
         assert_parity(ctx, arena, off + shift, ln, ALL | N.F_ACCEPT_ICMP)
+        assert_parity(ctx, arena, off + shift, ln, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP |
+                      N.F_CSUM_L4 | N.F_FLOW_HASH, fields=False)
 
 
 @pytest.mark.parametrize("slot,shift", [(16, 0), (64, 4), (256, 0), (64, 2)])
@@ -136,6 +144,10 @@ def test_checksum_tail_lengths(ctx, slot, shift):
     arena = np.concatenate([np.zeros(shift, np.uint8), arena])
     om = assert_parity(ctx, arena, off + shift, ln, ALL, fields=False)
     assert ((om & 0xFF) == 0).all() and (om & N.META_L4_CSUM_OK).all()
+    # the IPv4/UDP variant on the same frames (the others fail NOT_IPV4 / NOT_UDP)
+    om = assert_parity(ctx, arena, off + shift, ln, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP |
+                       N.F_CSUM_L4 | N.F_FLOW_HASH, fields=False)
+    assert (om & N.META_L4_CSUM_OK).sum() > 1000
 
 
 def test_packet_flush_with_arena_end(ctx):
@@ -316,4 +328,6 @@ def test_rows_path_long_frames(ctx, seed):
         arena, off, ln = synth.pack_frames(frames, slot)
         for flags in (ALL, ALL | N.F_ACCEPT_ICMP, N.F_ACCEPT_V6 | N.F_ACCEPT_TCP | N.F_CSUM_L4):
             om = assert_parity(ctx, arena, off, ln, flags, fields=True)
+        assert_parity(ctx, arena, off, ln, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP |
+                      N.F_CSUM_L4 | N.F_FLOW_HASH, fields=False)  # IPv4/UDP variant, rows
         assert (om & N.META_L4_CSUM_OK).sum() > 3000
