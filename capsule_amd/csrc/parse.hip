@@ -53,6 +53,9 @@ constexpr uint32_t kSlotIt = CGPU_SLOT_IT;  // slots per 16-lane row and round (
 #ifndef CGPU_PARSE_ROWS
 #define CGPU_PARSE_ROWS 1
 #endif
+#ifndef CGPU_PARSE_LINE0_MIN  // 0: off
+#define CGPU_PARSE_LINE0_MIN 1024
+#endif
 #ifndef CGPU_PARSE_ROW_MAX
 #define CGPU_PARSE_ROW_MAX 512
 #endif
@@ -292,6 +295,11 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
         P[4 * c + 2] = v[2];
         P[4 * c + 3] = v[3];
       }
+    } else if (V4U) {
+      // no frame of the wave reaches byte 64: in the IPv4/UDP variant these
+      // words are only read by the checksum sums, which skip or mask them
+#pragma unroll
+      for (int j = 16; j < kWin; ++j) P[j] = __builtin_nondeterministic_value(0u);
     } else {
 #pragma unroll
       for (int j = 16; j < kWin; ++j) P[j] = 0u;
@@ -460,7 +468,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     // pseudo-header addresses + span [l4, len) (udp.rs:204-219, tcp.rs:
     // 462-477, checksum.rs:56-128) are one contiguous byte range: [26, len)
     // for v4, [22, len) for v6; the stored checksum field is subtracted.
-    s = sad16(v6 ? (Q[5] & 0xffff0000u) : 0u, 0u);
+    s = V4U ? 0u : sad16(v6 ? (Q[5] & 0xffff0000u) : 0u, 0u);
     s = sad16(v6 ? Q[6] : (Q[6] & 0xffff0000u), s);
     const uint32_t endn = len - 4u * k;  // normalized end of frame
     // A span longer than the window is split at a 16-B aligned arena offset:
@@ -624,11 +632,31 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     // contiguous bytes per load) and reduced per frame.
     const uint32_t t_to = off + len;
     const uint32_t lane = threadIdx.x & 63u, grp = lane >> 4, l16 = lane & 15u;
+    uint32_t tail = 0;
+#if CGPU_PARSE_LINE0_MIN
+    // A long frame's tail would fetch the rest of the window's 128-B line
+    // again, after the 4 MB L2 has evicted it: its own lane sums those chunks
+    // now (at most 4, all inside the frame), and the tail starts on the next
+    // line.  Only for frames of CGPU_PARSE_LINE0_MIN bytes and more, where the
+    // kernel is bound by HBM bytes rather than by strided requests.
+    {
+      const uint32_t lb = (t_b + 127u) & ~127u;
+      const uint32_t nc = has_tail && len >= CGPU_PARSE_LINE0_MIN && lb < t_to ? (lb - t_b) >> 4 : 0u;
+      if (__ballot(nc != 0u)) {
+        u32x4 v[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j)
+          v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(j < nc ? t_b + 16u * j : kNoRead), 0, 0);
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) tail = sum4(v[j], tail);  // zeros where not loaded
+        t_b += 16u * (nc < 4u ? nc : 4u);
+      }
+    }
+#endif
     const uint32_t pieces = has_tail ? (t_to - t_b + 255u) >> 8 : 0u;  // 256-B pieces
     const bool slot_tail = has_tail && pieces <= kSlotPieces;
     // every chunk any tail needs lies inside the arena: branch-free loads
     const bool fast = !__ballot(has_tail && (uint64_t)((t_to + 15u) & ~15u) > (uint64_t)a.arena_len);
-    uint32_t tail = 0;
     // Short tails (one or two 256-B pieces): pass p sums piece p of every
     // frame that has one.  The frames of a pass are compacted (ds_permute of
     // their piece offset and end to lane rank), and a round takes 16 of
@@ -743,7 +771,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       for (uint32_t d = 8; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 16);
       const bool mine_now = long_tail && my_rank >= 4u * r && my_rank < 4u * r + 4u;
       const uint32_t got = __shfl(acc, mine_now ? (my_rank - 4u * r) * 16u : 0u);
-      if (mine_now) tail = got;
+      if (mine_now) tail += got;
     }
     if (has_tail) {
       uint32_t rt = fold32(tail);
