@@ -831,9 +831,6 @@ __device__ __forceinline__ void rows_build(const uint32_t (&D)[24], const uint32
 // Row-path cache policy of the frame loads and of the whole-row stores
 // (A/B knob: 2 = nontemporal; only the rows path writes whole lines per
 // instruction, so only it can use nontemporal stores without splitting them)
-#ifndef CGPU_NAT64_PROBE_AUX  // A/B knob: cache policy of the first slot load (-1: plain load)
-#define CGPU_NAT64_PROBE_AUX -1
-#endif
 #ifndef CGPU_NAT64_ROW_AUX
 #define CGPU_NAT64_ROW_AUX 0
 #endif
@@ -954,15 +951,9 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
 #ifndef CGPU_NAT64_ABL_NOPROBE
   if (act0) {
-#if CGPU_NAT64_PROBE_AUX >= 0
-    const rsrc_t ps = make_rsrc(a.pm.slots, 32u * (a.pm.cap_mask + 1u));
-    s0 = __builtin_amdgcn_raw_buffer_load_b128(ps, (int)(32u * h), 0, CGPU_NAT64_PROBE_AUX);
-    s1 = __builtin_amdgcn_raw_buffer_load_b128(ps, (int)(32u * h + 16u), 0, CGPU_NAT64_PROBE_AUX);
-#else
     const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
     s0 = sp[0];
     s1 = sp[1];
-#endif
   }
 #endif
   const uint32_t nl = len - 20u;  // meaningful for ACT frames
