@@ -240,6 +240,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   // --- the packet-relative window P ---------------------------------------
   uint32_t P[kWin];
   uint32_t wlim = 96u;  // packet bytes the window holds
+  uint32_t l0_sum = 0, l0_adv = 0;  // the window line's rest, summed early (below)
   bool rows = false;     // the rows path (above): window and frame sum from rows
   uint32_t s_all = 0;
 #if CGPU_PARSE_ROWS
@@ -295,6 +296,27 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
         P[4 * c + 2] = v[2];
         P[4 * c + 3] = v[3];
       }
+#if CGPU_PARSE_LINE0_MIN
+      // A long frame's checksum tail would start at (off + 64) & ~15 and
+      // fetch the rest of this 128-B line again, after the 4 MB L2 has
+      // evicted it: the lane sums those chunks now, with the window in
+      // flight (at most 4, all inside the frame), and the tail starts on the
+      // next line.  Frames of CGPU_PARSE_LINE0_MIN bytes and more only, where
+      // the kernel is bound by HBM bytes rather than by strided requests.
+      if (L4C) {
+        const uint32_t tb = (off + 64u) & ~15u, lb = (tb + 127u) & ~127u;
+        const uint32_t nc = wlim == 64u && len >= CGPU_PARSE_LINE0_MIN && lb < off + len ? (lb - tb) >> 4 : 0u;
+        if (__ballot(nc != 0u)) {
+          u32x4 v[4];
+#pragma unroll
+          for (uint32_t j = 0; j < 4u; ++j)
+            v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(j < nc ? tb + 16u * j : kNoRead), 0, 0);
+#pragma unroll
+          for (uint32_t j = 0; j < 4u; ++j) l0_sum = sum4(v[j], l0_sum);  // zeros where not loaded
+          l0_adv = 16u * (nc < 4u ? nc : 4u);
+        }
+      }
+#endif
     } else if (V4U) {
       // no frame of the wave reaches byte 64: in the IPv4/UDP variant these
       // words are only read by the checksum sums, which skip or mask them
@@ -634,14 +656,15 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     const uint32_t lane = threadIdx.x & 63u, grp = lane >> 4, l16 = lane & 15u;
     uint32_t tail = 0;
 #if CGPU_PARSE_LINE0_MIN
-    // A long frame's tail would fetch the rest of the window's 128-B line
-    // again, after the 4 MB L2 has evicted it: its own lane sums those chunks
-    // now (at most 4, all inside the frame), and the tail starts on the next
-    // line.  Only for frames of CGPU_PARSE_LINE0_MIN bytes and more, where the
-    // kernel is bound by HBM bytes rather than by strided requests.
+    // the window line's rest (see the window loads): summed early, or now
+    // (waves that took the general window loader)
+    if (l0_adv != 0u && has_tail) {
+      tail = l0_sum;
+      t_b += l0_adv;
+    }
     {
       const uint32_t lb = (t_b + 127u) & ~127u;
-      const uint32_t nc = has_tail && len >= CGPU_PARSE_LINE0_MIN && lb < t_to ? (lb - t_b) >> 4 : 0u;
+      const uint32_t nc = has_tail && l0_adv == 0u && len >= CGPU_PARSE_LINE0_MIN && lb < t_to ? (lb - t_b) >> 4 : 0u;
       if (__ballot(nc != 0u)) {
         u32x4 v[4];
 #pragma unroll
