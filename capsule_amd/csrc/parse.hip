@@ -54,7 +54,7 @@ constexpr uint32_t kSlotIt = CGPU_SLOT_IT;  // slots per 16-lane row and round (
 #define CGPU_PARSE_ROWS 1
 #endif
 #ifndef CGPU_PARSE_LINE0_MIN  // 0: off
-#define CGPU_PARSE_LINE0_MIN 1024
+#define CGPU_PARSE_LINE0_MIN 512
 #endif
 #ifndef CGPU_PARSE_ROW_MAX
 #define CGPU_PARSE_ROW_MAX 512
