@@ -323,9 +323,19 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None):
                                            direction) for k in range(2 * copies)]
     cycle = len(launchers)
 
+    # HIP events on the launch stream bracket the K timed launches (ev0 just
+    # before the first, ev1 behind the last): (ev1 - ev0) / K is the per-launch
+    # device time (kernel plus the back-to-back dispatch gap).  Both are
+    # recorded once here first: torch creates an event's HIP object at its
+    # first record, which must not happen inside the timed region.
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    ev1.record(stream)
+
     # warm-up: >= `warmup` launches and >= MIN_WARM_S of device time, issued
     # back to back (no host sync in between) so the clocks are at their
-    # steady state when the timed region starts
+    # steady state when the timed region starts; the region's own sync +
+    # barrier follow the last warm-up launch directly (no idle GPU between)
     k = 0
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -337,17 +347,7 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None):
     for _ in range(max(warmup, int(MIN_WARM_S / per) + 1)):
         launchers[k % cycle]()
         k += 1
-    torch.cuda.synchronize(dev)
 
-    # HIP events on the launch stream bracket the K timed launches (ev0 just
-    # before the first, ev1 behind the last): (ev1 - ev0) / K is the per-launch
-    # device time (kernel plus the back-to-back dispatch gap).  Both are
-    # recorded once here first: torch creates an event's HIP object at its
-    # first record, which must not happen inside the timed region.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
     state = {"k": k, "left": steps}
 
     def one():
