@@ -323,44 +323,55 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None):
                                            direction) for k in range(2 * copies)]
     cycle = len(launchers)
 
-    # HIP events on the launch stream bracket the K timed launches (ev0 just
-    # before the first, ev1 behind the last): (ev1 - ev0) / K is the per-launch
-    # device time (kernel plus the back-to-back dispatch gap).  Both are
-    # recorded once here first: torch creates an event's HIP object at its
-    # first record, which must not happen inside the timed region.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    ev1.record(stream)
+    # HIP events on the launch stream: eva behind the first timed launch, ev1
+    # behind the last; (ev1 - eva) / (K - 1) is the per-launch device time of
+    # launches 2..K (kernel plus the back-to-back dispatch gap), which the
+    # host keeps queued ahead of the device.  Nothing is recorded before the
+    # first launch, so the region starts with the launch itself; the first
+    # launch's submission latency is in ms_per_step, not in the kernel time.
+    # Both are recorded once here first: torch creates an event's HIP object
+    # at its first record, which must not happen inside the timed region.
+    eva, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for e in (eva, ev1):
+        e.record(stream)
 
-    # warm-up: >= `warmup` launches and >= MIN_WARM_S of device time, issued
-    # back to back (no host sync in between) so the clocks are at their
-    # steady state when the timed region starts; the region's own sync +
-    # barrier follow the last warm-up launch directly (no idle GPU between)
+    # warm-up: >= `warmup` launches and >= MIN_WARM_S of device time, in
+    # bursts of 64 back-to-back launches (a sync after each keeps the
+    # runtime's launch queue short), so the clocks are at their steady state;
+    # then two untimed rehearsals of the timed region's own shape (`steps`
+    # launches between syncs)
     k = 0
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(32):
-        launchers[k % cycle]()
-        k += 1
-    torch.cuda.synchronize(dev)
-    per = (time.perf_counter() - t0) / 32
-    for _ in range(max(warmup, int(MIN_WARM_S / per) + 1)):
-        launchers[k % cycle]()
-        k += 1
+    done = 0
+    while done < warmup or time.perf_counter() - t0 < MIN_WARM_S:
+        for _ in range(64):
+            launchers[k % cycle]()
+            k += 1
+        done += 64
+        torch.cuda.synchronize(dev)
+    for _ in range(2):
+        for _ in range(steps):
+            launchers[k % cycle]()
+            k += 1
+        torch.cuda.synchronize(dev)
 
     state = {"k": k, "left": steps}
 
     def one():
-        if state["left"] == steps:
-            ev0.record(stream)
         launchers[state["k"] % cycle]()
+        if state["left"] == steps:
+            eva.record(stream)
         state["k"] += 1
         state["left"] -= 1
         if state["left"] == 0:
             ev1.record(stream)
 
     elapsed = g.timed(one, steps, sync=lambda: torch.cuda.synchronize(dev))
-    kern_us = ev0.elapsed_time(ev1) / steps * 1e3
+    if steps > 1:
+        kern_us = eva.elapsed_time(ev1) / (steps - 1) * 1e3
+    else:  # one launch: eva and ev1 both follow it; fall back to the wall time
+        kern_us = elapsed / steps * 1e6
     res = dict(cfg=cfg, n=n, desc=w["desc"], frame=w["frame"], copies=copies, elapsed=elapsed,
                steps=steps, kern_us=kern_us, algo_bytes=w["algo_bytes"],
                achieved=w["algo_bytes"] / (kern_us * 1e-6) / 1e9, w=w)
@@ -502,9 +513,12 @@ def main():
     if args.e2e:
         return e2e(args)
     g = ShardGroup()
-    dev = torch.device("cuda", g.local_rank)
+    # CGPU_BENCH_ONE_DEVICE=1: every rank on GPU 0 (rehearsing the N-rank
+    # path on a one-GPU box; the ranks then share the card)
+    ordinal = 0 if os.environ.get("CGPU_BENCH_ONE_DEVICE") == "1" else g.local_rank
+    dev = torch.device("cuda", ordinal)
     torch.cuda.set_device(dev)
-    ctx = packets.Context(g.local_rank)
+    ctx = packets.Context(ordinal)
 
     main_r = bench_config(args.config, g, ctx, dev, args.steps, args.warmup)
     extra = {}
