@@ -778,9 +778,9 @@ __device__ __forceinline__ void quad_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
 // the output and at most 256 B long (one input pass), the wave moves its frames in rows of 16 lanes, four
 // whole frames per load and store instruction (full lines), and decides per
 // frame in one lane:
-//   A. each lane loads the first 96 B of its own frame, then row j loads
-//      frame 4r + j in round r, lane l its 16-B chunk l; while those loads
-//      are in flight each lane classifies its frame, probes the port map
+//   A. row j loads frame 4r + j in round r, lane l its 16-B chunk l; the
+//      rows pass bytes 0..95 of every frame through wave-private LDS to the
+//      frame's own lane, which classifies its frame, probes the port map
 //      (the probe's latency hides behind the row loads) and builds output
 //      bytes 0..63 (Ethernet, the IPv4 header, the start of the rewritten TCP
 //      header) and their part of the TCP sum into a wave-private LDS record;
@@ -793,6 +793,9 @@ __device__ __forceinline__ void quad_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
 // layout), one output length for the wave (per-lane chunk masks computed
 // once).
 constexpr uint32_t kRowW = 20;  // LDS dwords per frame record
+#ifndef CGPU_NAT64_ROW_DLDS  // classification bytes from the rows via LDS (0: own loads)
+#define CGPU_NAT64_ROW_DLDS 1
+#endif
 #ifndef CGPU_NAT64_ROW_FRAMES
 #define CGPU_NAT64_ROW_FRAMES 32
 #endif
@@ -920,13 +923,15 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   // (b128 stores at any dword: packed output frames stay on this path)
   if (__ballot(valid && ((off & 15u) != 0u || (o_off & 3u) != 0u || len > 256u))) return false;
   const uint32_t row = lane >> 4, l = lane & 15u;
-  // A1: this lane's own frame, input bytes 0..95, for the classification
   uint32_t D[24];
+#if !CGPU_NAT64_ROW_DLDS
+  // A1: this lane's own frame, input bytes 0..95, for the classification
 #pragma unroll
   for (uint32_t m = 0; m < 6u; ++m) {
     const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * m < len ? off + 16u * m : kNoRead), 0, kRowLdAux);
     D[4 * m] = t[0]; D[4 * m + 1] = t[1]; D[4 * m + 2] = t[2]; D[4 * m + 3] = t[3];
   }
+#endif
   // A2: the frames in rows, four whole frames per load instruction; in
   // flight while the headers are classified and the port map is probed
   u32x4 X[R];
@@ -936,6 +941,21 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     const uint32_t fo = __shfl(off, (int)f), fl = __shfl(len, (int)f);
     X[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * l < fl ? fo + 16u * l : kNoRead), 0, kRowLdAux);
   }
+#if CGPU_NAT64_ROW_DLDS
+  // A1: bytes 0..95 of every frame from its row, through wave-private LDS
+  // (the record area, not yet in use) to the frame's own lane: no strided
+  // per-lane loads of the header lines the rows have just fetched
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r)
+    if (l < 6u) *reinterpret_cast<u32x4 *>(lds + (4u * r + row) * 24u + 4u * l) = X[r];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+  for (uint32_t m = 0; m < 6u; ++m) {
+    const u32x4 t = *reinterpret_cast<const u32x4 *>(lds + (mine ? lane : 0u) * 24u + 4u * m);
+    D[4 * m] = t[0]; D[4 * m + 1] = t[1]; D[4 * m + 2] = t[2]; D[4 * m + 3] = t[3];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#endif
   uint32_t *rec = lds + (mine ? lane : 0u) * kRowW;
   // A3: the reference control flow; the first port-map slot of the key is
   // loaded now and examined after B1
@@ -1023,7 +1043,7 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
 }
 
 __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a) {
-  __shared__ uint32_t lds[kBlock / 64][kRowFrames * kRowW];
+  __shared__ uint32_t lds[kBlock / 64][kRowFrames * (kRowW > 24u ? kRowW : 24u)];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t base = (blockIdx.x * (kBlock / 64u) + wave) * kRowFrames;
   if (base >= a.n) return;  // wave-uniform
