@@ -56,6 +56,9 @@ constexpr uint32_t kSlotIt = CGPU_SLOT_IT;  // slots per 16-lane row and round (
 #ifndef CGPU_PARSE_LINE0_MIN  // 0: off
 #define CGPU_PARSE_LINE0_MIN 512
 #endif
+#ifndef CGPU_PARSE_ROWS_MEAN_MAX  // largest mean slot (arena bytes / packet) given the rows variant
+#define CGPU_PARSE_ROWS_MEAN_MAX 2200
+#endif
 #ifndef CGPU_PARSE_ROW_MAX
 #define CGPU_PARSE_ROW_MAX 512
 #endif
@@ -140,16 +143,17 @@ __device__ __forceinline__ uint32_t chunk_excess(u32x4 v, uint32_t c, uint32_t f
 }
 
 // ---- the rows path (L4 checksum configs, waves of long frames) -----------
-// A wave whose frames are 16-B aligned, at most 512 B long and mostly
-// (>= half) at least 128 B long reads each frame once, in rows: 16 lanes
+// A wave whose frames are 16-B aligned and at least half of them 128 B or
+// longer reads each frame's first 512 B once, in rows: 16 lanes
 // take one 256-B piece of one frame per load instruction (four whole frames
 // per instruction, full lines), sum its u16 words (the frame's last chunk
 // masked at its end) and reduce them over the row with DPP; the first 96 B
 // of every frame pass through wave-private LDS to the frame's own lane.  The
 // lane then has its window P and the exact word sum of the whole frame;
-// the checksum span's sum is that sum minus the words before the span.  No
-// line is fetched twice, as the per-lane window + tail passes do for line 0
-// of long frames (window: bytes 0..63; tail: bytes 64..127, later).
+// the checksum span's sum is that sum minus the words before the span, plus
+// the checksum tail's sum of bytes [512, len) for longer frames.  No line is
+// fetched twice, as the per-lane window + tail passes can for line 0 of long
+// frames (window: bytes 0..63; tail: bytes 64..127, later).
 // Frames are processed in two halves of 32 (LDS: 32 x 96 B + sums per wave).
 constexpr uint32_t kRowHalf = 32;
 constexpr uint32_t kRowLds = kRowHalf * kWin + kRowHalf;  // dwords per wave
@@ -157,7 +161,10 @@ constexpr uint32_t kRowLds = kRowHalf * kWin + kRowHalf;  // dwords per wave
 __device__ __forceinline__ void rows_prologue(rsrc_t rs, uint32_t off, uint32_t len, uint32_t lane,
                                               uint32_t *L, uint32_t (&P)[kWin], uint32_t &s_all) {
   const uint32_t row = lane >> 4, l = lane & 15u;
-  uint32_t npass = 0;  // 256-B pieces of the wave's longest frame
+  // a frame longer than kRowMaxLen is summed here up to kRowMaxLen; the
+  // checksum tail takes the rest
+  len = len < kRowMaxLen ? len : kRowMaxLen;
+  uint32_t npass = 0;  // 256-B pieces of the wave's longest (clipped) frame
 #pragma unroll
   for (uint32_t p = 0; p < kRowMaxLen / 256u; ++p)
     if (__ballot(len > 256u * p)) npass = p + 1u;
@@ -245,8 +252,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   uint32_t s_all = 0;
 #if CGPU_PARSE_ROWS
   if (ROWS) {
-    const bool bad = valid && ((off & 15u) != 0u || len > kRowMaxLen ||
-                               (uint64_t)off + len + 16u > (uint64_t)a.arena_len);
+    const bool bad = valid && ((off & 15u) != 0u || (uint64_t)off + len + 16u > (uint64_t)a.arena_len);
     const uint64_t vm = __ballot(valid);
     rows = vm && !__ballot(bad) &&
            2u * (uint32_t)__popcll(__ballot(valid && len >= 128u)) >= (uint32_t)__popcll(vm);
@@ -485,6 +491,8 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
                        : (v6 ? (Q[17] >> 16) : (Q[12] >> 16));
     s -= stored_le;
     if (icmp && !v6) s -= (Q[6] >> 16) + (Q[7] & 0xffffu) + (Q[7] >> 16) + (Q[8] & 0xffffu);
+    has_tail = len > kRowMaxLen;  // the rows summed bytes [0, kRowMaxLen)
+    t_b = off + kRowMaxLen;       // 16-B aligned: rows frames are
   }
   if (L4C && l4_ok && (!(ROWS && rows) || xok)) {
     // pseudo-header addresses + span [l4, len) (udp.rs:204-219, tcp.rs:
@@ -820,10 +828,10 @@ template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT, bool V4U>
 hipError_t launch_t(const ParseArgs &a, hipStream_t s) {
   const uint32_t grid = (a.n + kBlock - 1) / kBlock;
   // The rows path is compiled into a variant that the checksum configs get
-  // when the batch's mean slot (arena bytes per packet) is 128..640 B: long
+  // when the batch's mean slot (arena bytes per packet) is 128..2200 B: long
   // frames, but not jumbo ones; each wave still decides by its own frames.
   const uint64_t mean = (uint64_t)a.arena_len / a.n;
-  if (L4C && CGPU_PARSE_ROWS && mean >= 128u && mean <= 640u)
+  if (L4C && CGPU_PARSE_ROWS && mean >= 128u && mean <= CGPU_PARSE_ROWS_MEAN_MAX)
     hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, V4U, true>), dim3(grid), dim3(kBlock), 0, s, a);
   else
     hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, V4U, false>), dim3(grid), dim3(kBlock), 0, s, a);
