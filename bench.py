@@ -278,7 +278,7 @@ def pmc_traffic(cfg):
     return None
 
 
-def bench_config(cfg, g, ctx, dev, steps, warmup, w=None):
+def bench_config(cfg, g, ctx, dev, steps, warmup, w=None, queues=1):
     """Time one config on this rank.
 
     Builds the rank's shard of the workload, keeps R copies resident in HBM
@@ -287,6 +287,11 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None):
     device time, then times `steps` launches between a sync + barrier on
     each side (ShardGroup.timed: max over ranks).  HIP events recorded on the
     launch stream around the same launches give the per-launch device time.
+
+    queues > 1 (parse configs): the rank serves that many RX queues, each on
+    its own HIP stream with its own outputs, launch k on queue k mod queues;
+    consecutive launches then overlap, so there is no per-launch device time
+    and the rate comes from the wall clock alone.
     """
     import torch
 
@@ -301,12 +306,14 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None):
     batches = [b0] + [packets.PacketBatch(b0.arena.clone(), b0.off.clone(), b0.len.clone())
                       for _ in range(copies - 1)]
     stream = torch.cuda.current_stream(dev)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(queues - 1)]
     if w["kind"] == "parse":
         # checksum verify: CSUM_OK bits in meta, computed values not stored
-        outs = [packets.ParseBuffers(n, dev, csum=False) for _ in range(2)]
-        launchers = [packets.ParseLauncher(ctx, batches[k % copies], outs[k & 1], w["flags"],
-                                           stream) for k in range(2 * copies)]
+        outs = [packets.ParseBuffers(n, dev, csum=False) for _ in range(max(2, queues))]
+        launchers = [packets.ParseLauncher(ctx, batches[k % copies], outs[k % len(outs)], w["flags"],
+                                           streams[k % queues]) for k in range(2 * copies * queues)]
     else:
+        assert queues == 1, "one port map, one queue"
         direction = "4to6" if gw is not None else "6to4"
         gw = gw or packets.Nat64Gateway(ctx, capacity_log2=PORTMAP_LOG2)
         if "out_off" in w:
@@ -368,11 +375,13 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None):
             ev1.record(stream)
 
     elapsed = g.timed(one, steps, sync=lambda: torch.cuda.synchronize(dev))
-    if steps > 1:
+    if queues > 1:  # launches overlap across the queues: wall clock only
+        kern_us = elapsed / steps * 1e6
+    elif steps > 1:
         kern_us = eva.elapsed_time(ev1) / (steps - 1) * 1e3
     else:  # one launch: eva and ev1 both follow it; fall back to the wall time
         kern_us = elapsed / steps * 1e6
-    res = dict(cfg=cfg, n=n, desc=w["desc"], frame=w["frame"], copies=copies, elapsed=elapsed,
+    res = dict(cfg=cfg, n=n, desc=w["desc"], frame=w["frame"], copies=copies, elapsed=elapsed, queues=queues,
                steps=steps, kern_us=kern_us, algo_bytes=w["algo_bytes"],
                achieved=w["algo_bytes"] / (kern_us * 1e-6) / 1e9, w=w)
     del launchers, outs, batches, b0
@@ -540,6 +549,18 @@ def main():
                     r["w"] = None
             extra["sizes"] = sizes
         shard_r["w"] = None if shard_r is not main_r else shard_r["w"]
+        if g.world == 1 and main_r["w"]["kind"] == "parse":
+            # the same workload served as two RX queues of this GPU (two
+            # streams, launches alternating): the chip's rate when launches
+            # overlap instead of draining one by one (context for `value`,
+            # which stays one queue per GPU)
+            q = bench_config(args.config, g, ctx, dev, sub, args.warmup, w=main_r["w"], queues=2)
+            extra["rx_queues"] = {
+                "queues": 2, "mpps": round(q["n"] * q["steps"] / q["elapsed"] / 1e6, 2),
+                "us_per_launch_wall": round(q["kern_us"], 3),
+                "achieved_GBps": round(q["achieved"], 1),
+                "frac": round(q["achieved"] / HBM_PEAK_GBS, 4),
+                "basis": "algorithmic bytes per launch / wall time per launch (launches overlap)"}
     cpu = None
     if g.world == 1 and not args.no_cpu:
         cpu = cpu_baseline(main_r["w"], args.cpu_seconds)
@@ -684,6 +705,7 @@ def e2e(args):
             host_out[d][1].copy_(outs[d].flow_hash, non_blocking=True)
         down_bytes = 12 * n
     else:
+        assert queues == 1, "one port map, one queue"
         direction = "4to6" if gw is not None else "6to4"
         gw = gw or packets.Nat64Gateway(ctx, capacity_log2=17)
         nat = [(torch.empty_like(bufs[d].arena), bufs[d].off,
