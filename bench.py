@@ -494,8 +494,10 @@ def main():
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--e2e", action="store_true",
                     help="host-resident batches: pinned H2D + parse + D2H, pipelined (DESIGN.md §8)")
-    ap.add_argument("--ingress", choices=["stage", "zero_copy"],
-                    help="with --e2e: rte_mbuf bursts from a host mempool through cgpu_parse_mbufs")
+    ap.add_argument("--ingress", choices=["stage", "zero_copy", "frames"],
+                    help="with --e2e: rte_mbuf bursts from a host mempool through cgpu_parse_mbufs "
+                         "(stage / zero_copy) or as (address, length) pairs through "
+                         "cgpu_parse_frames (frames, zero-copy)")
     ap.add_argument("--burst", type=int, default=1 << 18,
                     help="with --ingress: mbufs per cgpu_parse_mbufs call")
     args = ap.parse_args()
@@ -635,16 +637,28 @@ def e2e_mbufs(args):
     pinned = torch.zeros(stride * n, dtype=torch.uint8, pin_memory=True)
     mem, mbufs = synth.mbuf_pool(w["arena"], w["off"], w["len"], mem=pinned.numpy())
     reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
-    ingress = {"stage": N.INGRESS_STAGE, "zero_copy": N.INGRESS_ZERO_COPY}[args.ingress]
+    ingress = {"stage": N.INGRESS_STAGE, "zero_copy": N.INGRESS_ZERO_COPY,
+               "frames": N.INGRESS_ZERO_COPY}[args.ingress]
     B = min(args.burst, n)
     bursts = [mbufs[s:s + B] for s in range(0, n - B + 1, B)]
     outs = [(np.zeros(B, np.uint32), np.zeros(B, np.uint32), np.zeros(B, np.uint64))
             for _ in range(2)]
     L = N.lib()
+    if args.ingress == "frames":
+        # the RX core hands over (data_address, data_len) pairs, read from the
+        # mbuf headers it has just written (outside the timed calls)
+        fa, fl = synth.mbuf_frames(mem, mbufs)
+        pairs = [(fa[s:s + B].copy(), fl[s:s + B].copy()) for s in range(0, n - B + 1, B)]
 
     def call(k):  # the device-resident config's work: parse + checksums + hash
-        mb = bursts[k % len(bursts)]
         meta, cs, fh = outs[k & 1]
+        if args.ingress == "frames":
+            a, ln = pairs[k % len(pairs)]
+            N.check(L.cgpu_parse_frames(ctx.handle, a.ctypes.data, ln.ctypes.data, B, w["flags"],
+                                        ingress, meta.ctypes.data, cs.ctypes.data, fh.ctypes.data,
+                                        None), "cgpu_parse_frames")
+            return
+        mb = bursts[k % len(bursts)]
         N.check(L.cgpu_parse_mbufs(ctx.handle, mb.ctypes.data, B, w["flags"], ingress,
                                    meta.ctypes.data, cs.ctypes.data, fh.ctypes.data, None),
                 "cgpu_parse_mbufs")
@@ -657,7 +671,9 @@ def e2e_mbufs(args):
         calls += 1
     el = time.perf_counter() - t0
     print(json.dumps({
-        "metric": "end-to-end Mpps, rte_mbuf bursts from a host mempool (cgpu_parse_mbufs)",
+        "metric": "end-to-end Mpps, rte_mbuf bursts from a host mempool ("
+                  + ("cgpu_parse_frames: (data_address, data_len) pairs, zero-copy"
+                     if args.ingress == "frames" else "cgpu_parse_mbufs") + ")",
         "value": round(calls * B / el / 1e6, 2), "unit": "Mpps", "config": args.config,
         "ingress": args.ingress, "burst": B, "calls": calls,
         "us_per_burst": round(el / calls * 1e6, 1),

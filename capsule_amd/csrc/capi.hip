@@ -372,6 +372,8 @@ hipError_t gather_chunk(cgpu_ctx *ctx, const uint64_t *ptrs, uint32_t m, uint8_t
   if (hipMemsetAsync(cnt, 0, sizeof(ZcCounters), s) != hipSuccess) return hipErrorUnknown;
   cgpu::GatherArgs g;
   g.mbufs = ptrs;
+  g.frames = nullptr;
+  g.flen = nullptr;
   g.n = m;
   g.nreg = ctx->nreg;
   for (uint32_t r = 0; r < cgpu::kMaxRegions; ++r) g.reg[r] = ctx->reg[r];
@@ -390,6 +392,31 @@ hipError_t gather_chunk(cgpu_ctx *ctx, const uint64_t *ptrs, uint32_t m, uint8_t
     g.pkt_len = (uint32_t *)(g.fr_dev + stride);
     g.tailroom = g.pkt_len + stride;
   }
+  return cgpu::launch_mbuf_gather(g, s);
+}
+
+// The same gather from (frame address, length) pairs (device copies at
+// `frames` / `flen`).
+hipError_t gather_frames_chunk(cgpu_ctx *ctx, const uint64_t *frames, const uint16_t *flen,
+                               uint32_t m, uint8_t *arena, size_t arena_cap, uint32_t *off,
+                               uint16_t *len, ZcCounters *cnt, hipStream_t s) {
+  if (hipMemsetAsync(cnt, 0, sizeof(ZcCounters), s) != hipSuccess) return hipErrorUnknown;
+  cgpu::GatherArgs g;
+  g.mbufs = nullptr;
+  g.frames = frames;
+  g.flen = flen;
+  g.n = m;
+  g.nreg = ctx->nreg;
+  for (uint32_t r = 0; r < cgpu::kMaxRegions; ++r) g.reg[r] = ctx->reg[r];
+  g.arena = arena;
+  g.arena_cap = arena_cap;
+  g.off = off;
+  g.len = len;
+  g.cursor = &cnt->cursor;
+  g.bad = &cnt->bad;
+  g.slot_extra = 0;
+  g.mb_dev = g.fr_dev = nullptr;
+  g.pkt_len = g.tailroom = nullptr;
   return cgpu::launch_mbuf_gather(g, s);
 }
 
@@ -445,6 +472,56 @@ static int parse_zero_copy(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32
   return bad_total ? fail(CGPU_EINVAL) : ok();
 }
 
+// Zero-copy from (frame address, length) pairs: as parse_zero_copy, with the
+// pairs uploaded instead of mbuf pointers and no mbuf header read.
+static int parse_frames_zero_copy(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *len,
+                                  uint32_t n, uint32_t flags, uint32_t *meta, uint32_t *csum,
+                                  uint64_t *flow_hash, cgpu_hdr_record *fields) {
+  if (ctx->nreg == 0) return fail(CGPU_EINVAL);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
+  const uint32_t m0 = n < kZcChunk ? n : kZcChunk;
+  if (int e = grow_dev(&ctx->d_zc, &ctx->zc_cap, (size_t)m0 * kZcSlot + 64)) return fail(e);
+  const size_t ptrs = 0, lens = align_up(8ull * m0, 256), counters = lens + align_up(2ull * m0, 256);
+  const HostLayout lay(m0, fields != nullptr, counters + 256);
+  if (int e = grow(&ctx->h_desc, &ctx->d_desc, &ctx->desc_cap, lay.end)) return fail(e);
+  hipStream_t s = ctx->stream;
+  uint8_t *D = ctx->d_desc, *H = ctx->h_desc;
+  ZcCounters *dcnt = (ZcCounters *)(D + counters), *hcnt = (ZcCounters *)(H + counters);
+  uint32_t bad_total = 0;
+  for (uint32_t at = 0; at < n;) {
+    uint32_t m = n - at < m0 ? n - at : m0;
+    for (;;) {
+      memcpy(H + ptrs, pkt + at, 8ull * m);
+      memcpy(H + lens, len + at, 2ull * m);
+      if (hipMemcpyAsync(D + ptrs, H + ptrs, lens + 2ull * m, hipMemcpyHostToDevice, s) != hipSuccess)
+        return fail(CGPU_EIO);
+      const size_t cap = ctx->zc_cap < kZcArenaMax ? ctx->zc_cap : kZcArenaMax;
+      if (gather_frames_chunk(ctx, (const uint64_t *)(D + ptrs), (const uint16_t *)(D + lens), m,
+                              ctx->d_zc, cap, (uint32_t *)(D + lay.off), (uint16_t *)(D + lay.len),
+                              dcnt, s) != hipSuccess)
+        return fail(CGPU_EIO);
+      if (int e = parse_and_return(ctx, ctx->d_zc, cap, m, lay, flags, meta, csum, flow_hash,
+                                   fields, at))
+        return e;
+      if (hipMemcpyAsync(hcnt, dcnt, sizeof(ZcCounters), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+        return fail(CGPU_EIO);
+      const uint64_t need = hcnt->cursor + 64;
+      if (need <= cap) break;
+      if (need > kZcArenaMax) {  // fewer frames in this chunk
+        m = (uint32_t)((uint64_t)m * (kZcArenaMax / 2) / need);
+        if (m == 0) m = 1;
+        continue;
+      }
+      if (int e = grow_dev(&ctx->d_zc, &ctx->zc_cap, need)) return fail(e);
+    }
+    bad_total += hcnt->bad;
+    at += m;
+  }
+  return bad_total ? fail(CGPU_EINVAL) : ok();
+}
+
 extern "C" {
 
 int cgpu_parse_host(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *len, uint32_t n,
@@ -459,6 +536,18 @@ int cgpu_parse_host(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *le
     return p != nullptr || l == 0;
   };
   return parse_staged(ctx, n, get, flags, meta, csum, flow_hash, fields);
+}
+
+int cgpu_parse_frames(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *len, uint32_t n,
+                      uint32_t flags, uint32_t ingress, uint32_t *meta, uint32_t *csum,
+                      uint64_t *flow_hash, cgpu_hdr_record *fields) {
+  if (!ctx) return fail(CGPU_EINVAL);
+  if (n == 0) return ok();
+  if (!pkt || !len || !meta) return fail(CGPU_EINVAL);
+  if (ingress == CGPU_INGRESS_ZERO_COPY)
+    return parse_frames_zero_copy(ctx, pkt, len, n, flags, meta, csum, flow_hash, fields);
+  if (ingress != CGPU_INGRESS_STAGE) return fail(CGPU_EINVAL);
+  return cgpu_parse_host(ctx, pkt, len, n, flags, meta, csum, flow_hash, fields);
 }
 
 int cgpu_host_register(cgpu_ctx *ctx, void *base, size_t bytes) {

@@ -9,7 +9,9 @@
 // buf_addr + data_off .. + data_len, first segment only, as Mbuf::data_len /
 // data_address / read_data (core/src/dpdk/mbuf.rs:196-205, 313-327).
 //
-// Quads of lanes read the mbuf headers (one 64-B request per mbuf), the wave
+// Quads of lanes read the mbuf headers (one 64-B request per mbuf) -- or the
+// caller hands over (data_address, data_len) pairs and no header is read --
+// the wave
 // allocates its slots with one atomic, and then 16-lane groups copy four
 // frames at a time, 16 B per lane, all of a wave's first-256-B loads in
 // flight before any store.  Every host address is translated through the
@@ -51,10 +53,9 @@ __device__ __forceinline__ u32x4 load_host16(uint64_t dev, uint32_t avail) {
   return v;
 }
 
-__global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t lane = threadIdx.x & 63u;
-  const bool valid = i < g.n;
+// The frame of mbuf i: buf_addr + data_off, data_len, checked and translated.
+__device__ __forceinline__ void mbuf_frame(const GatherArgs &g, uint32_t i, uint32_t lane, bool valid,
+                                           uint64_t &src, uint32_t &L) {
   // --- the mbuf header: buf_addr @0, data_off @16, data_len @40 --------------
   // Read cooperatively: in round r the quad of lanes 4m..4m+3 loads bytes
   // 0..47 of mbuf 16r + m as three 16-B pieces of one 64-B segment (one PCIe
@@ -93,8 +94,8 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
       blen = d52 >> 16;
     }
   }
-  uint64_t src = 0;
-  uint32_t L = 0;
+  src = 0;
+  L = 0;
   bool ok = false;
   if (mok) {
     // the frame lies in its own buffer (data_off + data_len <= buf_len, the
@@ -110,6 +111,24 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
     g.fr_dev[i] = src;
     g.pkt_len[i] = plen;
     g.tailroom[i] = (blen - doff - dlen) & 0xffffu;  // u16 arithmetic, as Mbuf::tailroom
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool valid = i < g.n;
+  uint64_t src = 0;
+  uint32_t L = 0;
+  if (g.frames) {
+    // (data_address, data_len) pairs from the RX core: the frame alone, one
+    // request per 64 B of frame, no mbuf header line
+    const uint32_t fl = valid ? g.flen[i] : 0u;
+    const bool ok = valid && (fl == 0u || translate(g, g.frames[i], fl, src));
+    if (valid && !ok) atomicAdd(g.bad, 1u);
+    L = ok ? fl : 0u;
+  } else {
+    mbuf_frame(g, i, lane, valid, src, L);
   }
   if (!g.arena) return;  // validate only (wave-uniform)
   // --- slots: one atomic per wave, prefix within the wave ---------------------

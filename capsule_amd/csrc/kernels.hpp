@@ -89,6 +89,8 @@ struct HostRegion {
 constexpr uint32_t kMaxRegions = 16;
 struct GatherArgs {
   const uint64_t *mbufs;  // [n] host rte_mbuf addresses (device copy of the array)
+  const uint64_t *frames; // or, when not null: [n] host frame addresses (data_address),
+  const uint16_t *flen;   //   [n] their lengths (data_len); no mbuf header is read
   uint32_t n;
   uint32_t nreg;
   HostRegion reg[kMaxRegions];

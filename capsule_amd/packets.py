@@ -255,6 +255,27 @@ def parse_mbufs(ctx, mbufs, flags=None, ingress=N.INGRESS_STAGE, fields=False):
     return meta, csum, fh, recs
 
 
+def parse_frames(ctx, addrs, lens, flags=None, ingress=N.INGRESS_STAGE, fields=False):
+    """A burst handed over as host (data_address, data_len) pairs (u64 and
+    u16 numpy arrays) parsed into host arrays.  INGRESS_ZERO_COPY: the device
+    reads the frames alone from registered host memory."""
+    if flags is None:
+        flags = parse_flags()
+    addrs = np.ascontiguousarray(addrs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    n = len(addrs)
+    meta = np.zeros(n, np.uint32)
+    csum = np.zeros(n, np.uint32)
+    fh = np.zeros(n, np.uint64)
+    fl = np.zeros((n, N.HDR_RECORD_SIZE), np.uint8) if fields else None
+    rc = N.lib().cgpu_parse_frames(
+        ctx.handle, addrs.ctypes.data, lens.ctypes.data, n, flags, ingress, meta.ctypes.data,
+        csum.ctypes.data, fh.ctypes.data, fl.ctypes.data if fields else None)
+    N.check(rc, "cgpu_parse_frames")
+    recs = fl.view(np.dtype(N.HDR_RECORD_FIELDS)).reshape(-1) if fields else None
+    return meta, csum, fh, recs
+
+
 class Groups:
     """Result of `group_by`: `idx[off[k]:off[k+1]]` are arm k's packets."""
 

@@ -430,3 +430,17 @@ def mbuf_pool(arena, off, length, mem=None, headroom=128, seed=7, room=None):
         intra = np.arange(T, dtype=np.int64) - start
         mem[np.repeat(dst0[c:c + (1 << 16)], L) + intra] = arena[np.repeat(src0[c:c + (1 << 16)], L) + intra]
     return mem, (np.uint64(base) + objs.astype(np.uint64)).astype(np.uint64)
+
+
+def mbuf_frames(mem, mbufs):
+    """(data_address u64[n], data_len u16[n]) of each mbuf of `mem`, read from
+    its header (buf_addr @0 + data_off @16, data_len @40): the pairs an RX
+    core hands to cgpu_parse_frames."""
+    o = (np.asarray(mbufs, dtype=np.uint64) - np.uint64(mem.ctypes.data)).astype(np.int64)
+    buf = np.zeros(len(o), np.uint64)
+    for b in range(8):
+        buf |= mem[o + b].astype(np.uint64) << np.uint64(8 * b)
+    doff = mem[o + 16].astype(np.uint64) | (mem[o + 17].astype(np.uint64) << np.uint64(8))
+    dlen = mem[o + 40].astype(np.uint16) | (mem[o + 41].astype(np.uint16) << np.uint16(8))
+    return buf + doff, dlen
+

@@ -276,6 +276,18 @@ int cgpu_parse_mbufs(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32_t fla
                      uint32_t ingress, uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
                      cgpu_hdr_record *fields);
 
+/* Parse a burst of n frames handed over as host (address, length) pairs --
+ * each mbuf's data_address / data_len (mbuf.rs:196-205), which the RX core
+ * has in cache right after rte_eth_rx_burst; outputs as cgpu_parse_host, in
+ * HOST arrays.  STAGE: the calling core gathers (= cgpu_parse_host).
+ * ZERO_COPY: the device reads the frames alone from regions registered with
+ * cgpu_host_register -- no mbuf header line per packet, as
+ * cgpu_parse_mbufs must read; a frame outside every registered region fails
+ * the call with CGPU_EINVAL (nothing is read through it).  Synchronous.   */
+int cgpu_parse_frames(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *len, uint32_t n,
+                      uint32_t flags, uint32_t ingress, uint32_t *meta, uint32_t *csum,
+                      uint64_t *flow_hash, cgpu_hdr_record *fields);
+
 /* ---- examples/nat64 6to4 -------------------------------------------------
  * Stateful IPv6 -> IPv4 rewrite of examples/nat64/main.rs:121-150, with the
  * port map of :37-53 held on the device.  NEXT_PORT starts at `first_port`

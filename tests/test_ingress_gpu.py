@@ -193,3 +193,45 @@ def test_zero_copy_rejects_frame_past_its_buffer(ctx):
         check(ctx, a, o, l, mbufs, N.INGRESS_ZERO_COPY, fields=False)
     finally:
         reg.close()
+
+
+@pytest.mark.parametrize("ingress", MODES)
+def test_frames_pairs_match_oracle(ctx, ingress):
+    """cgpu_parse_frames: the same burst handed over as (data_address,
+    data_len) pairs; zero-copy reads the frames alone from the registered
+    mempool (no mbuf header)."""
+    a, o, l = edge_batch(seed=23)
+    mem, mbufs = synth.mbuf_pool(a, o, l)
+    addrs, lens = synth.mbuf_frames(mem, mbufs)
+    assert (lens == l).all()
+    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    try:
+        gm, gc, gh, gf = packets.parse_frames(ctx, addrs, lens, ALL, ingress, fields=True)
+    finally:
+        reg.close()
+    om, oc, oh, of = oracle_lib.parse_batch(a, o, l, ALL, fields=True)
+    assert (gm == om).all(), np.nonzero(gm != om)[0][:8]
+    assert (gc == oc).all() and (gh == oh).all()
+    assert (gf.view(np.uint8).reshape(len(o), -1) == of).all()
+
+
+def test_frames_zero_copy_rejects_unregistered(ctx):
+    """A frame address outside every registered region fails the call and is
+    never read through."""
+    a, o, l = synth.imix(512, seed=5)
+    mem, mbufs = synth.mbuf_pool(a, o, l)
+    addrs, lens = synth.mbuf_frames(mem, mbufs)
+    other = np.zeros(4096, np.uint8)
+    addrs = addrs.copy()
+    addrs[100] = np.uint64(other.ctypes.data)
+    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    try:
+        with pytest.raises(N.CgpuError):
+            packets.parse_frames(ctx, addrs, lens, ALL, N.INGRESS_ZERO_COPY)
+        # the context stays usable
+        addrs[100] = synth.mbuf_frames(mem, mbufs)[0][100]
+        gm = packets.parse_frames(ctx, addrs, lens, ALL, N.INGRESS_ZERO_COPY)[0]
+        assert (gm == oracle_lib.parse_batch(a, o, l, ALL)[0]).all()
+    finally:
+        reg.close()
+
