@@ -593,20 +593,34 @@ def bench_nat64_mbufs(args, w):
     gw = packets.Nat64Gateway(ctx, capacity_log2=17)
     B = min(args.burst, n)
     bursts = [mbufs[s:s + B] for s in range(0, n - B + 1, B)]
-    gw.nat_mbufs(bursts[0], "6to4")  # first sight of the keys (deferred path), untimed
+    frames = args.ingress == "frames"
+    if frames:  # (data_address, data_len) pairs, as the RX core hands them over
+        fa, fl = synth.mbuf_frames(mem, mbufs)
+        pairs = [(fa[s:s + B].copy(), fl[s:s + B].copy()) for s in range(0, n - B + 1, B)]
+
+    def call(k):
+        if frames:
+            _, d, _ = gw.nat_frames(*pairs[k % len(pairs)], direction="6to4")
+            return d
+        return gw.nat_mbufs(bursts[k % len(bursts)], "6to4")[0]
+
+    call(0)  # first sight of the keys (deferred path), untimed
     calls, el, acts = 0, 0.0, 0
     while calls < max(4, args.steps // 50) or el < 1.0:
         np.copyto(mem, orig)
         t0 = time.perf_counter()
-        disp, _ = gw.nat_mbufs(bursts[calls % len(bursts)], "6to4")
+        disp = call(calls)
         el += time.perf_counter() - t0
         acts += int((disp == 0).sum())
         calls += 1
     print(json.dumps({
-        "metric": "end-to-end Mpps, nat64 6to4 over rte_mbuf bursts (cgpu_nat64_mbufs: "
-                  "zero-copy gather, rewrite, frames written back into the mbufs)",
+        "metric": "end-to-end Mpps, nat64 6to4 over rte_mbuf bursts (" +
+                  ("cgpu_nat64_frames: (data_address, data_len) pairs, frames rewritten in "
+                   "place, data_len left to the caller" if frames else
+                   "cgpu_nat64_mbufs: zero-copy gather, rewrite, frames written back into the "
+                   "mbufs") + ")",
         "value": round(calls * B / el / 1e6, 2), "unit": "Mpps", "config": args.config,
-        "ingress": "zero_copy", "burst": B, "calls": calls, "act_frac": round(acts / (calls * B), 4),
+        "ingress": args.ingress, "burst": B, "calls": calls, "act_frac": round(acts / (calls * B), 4),
         "us_per_burst": round(el / calls * 1e6, 1),
         "mempool": f"{n} objects x {stride} B, page-locked, shuffled; 128-B rte_mbuf headers"}),
         flush=True)
@@ -627,7 +641,7 @@ def e2e_mbufs(args):
 
     torch.cuda.set_device(0)
     w = make_workload(args.config, 0xC0FFEE + 2)
-    if w["kind"] == "nat64" and args.config == "nat64" and args.ingress == "zero_copy":
+    if w["kind"] == "nat64" and args.config == "nat64" and args.ingress in ("zero_copy", "frames"):
         return bench_nat64_mbufs(args, w)
     if w["kind"] != "parse":
         raise SystemExit("--ingress applies to the parse configs and to nat64 (zero_copy)")

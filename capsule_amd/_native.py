@@ -127,6 +127,7 @@ EXPORTS = [
     "cgpu_portmap_size", "cgpu_nat64_6to4", "cgpu_nat64_4to6", "cgpu_group_by", "cgpu_last_error", "cgpu_strerror",
     "cgpu_pkt_status_str", "cgpu_abi_version", "cgpu_host_register", "cgpu_host_unregister",
     "cgpu_parse_mbufs", "cgpu_set_ip", "cgpu_nat64_mbufs", "cgpu_parse_frames",
+    "cgpu_nat64_frames",
 ]
 
 _lib = None
@@ -176,6 +177,8 @@ def lib():
     L.cgpu_host_unregister.argtypes = [vp, vp]
     L.cgpu_parse_mbufs.restype = i32
     L.cgpu_parse_mbufs.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp, vp]
+    L.cgpu_nat64_frames.restype = i32
+    L.cgpu_nat64_frames.argtypes = [vp, vp, u32, vp, vp, vp, u32, vp, vp, vp]
     L.cgpu_parse_frames.restype = i32
     L.cgpu_parse_frames.argtypes = [vp, vp, vp, u32, u32, u32, vp, vp, vp, vp]
     L.cgpu_group_by.restype = i32

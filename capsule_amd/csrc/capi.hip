@@ -365,15 +365,19 @@ struct ZcCounters {  // device counters of one gather (16 bytes)
 
 // One zero-copy gather of mbufs[at, at + m) (the pointer array already at
 // `ptrs` on the device).  arena = nullptr: validate the pointers only.
+// frames != nullptr: `ptrs` is unused and the burst is (frames, flen) pairs,
+// with ftail the frames' tailrooms for the egress records.
 hipError_t gather_chunk(cgpu_ctx *ctx, const uint64_t *ptrs, uint32_t m, uint8_t *arena,
                         size_t arena_cap, uint32_t *off, uint16_t *len, ZcCounters *cnt,
                         uint32_t slot_extra, uint8_t *egress_base, uint32_t stride,
-                        hipStream_t s) {
+                        hipStream_t s, const uint64_t *frames = nullptr,
+                        const uint16_t *flen = nullptr, const uint16_t *ftail = nullptr) {
   if (hipMemsetAsync(cnt, 0, sizeof(ZcCounters), s) != hipSuccess) return hipErrorUnknown;
   cgpu::GatherArgs g;
-  g.mbufs = ptrs;
-  g.frames = nullptr;
-  g.flen = nullptr;
+  g.mbufs = frames ? nullptr : ptrs;
+  g.frames = frames;
+  g.flen = flen;
+  g.ftail = ftail;
   g.n = m;
   g.nreg = ctx->nreg;
   for (uint32_t r = 0; r < cgpu::kMaxRegions; ++r) g.reg[r] = ctx->reg[r];
@@ -405,6 +409,7 @@ hipError_t gather_frames_chunk(cgpu_ctx *ctx, const uint64_t *frames, const uint
   g.mbufs = nullptr;
   g.frames = frames;
   g.flen = flen;
+  g.ftail = nullptr;
   g.n = m;
   g.nreg = ctx->nreg;
   for (uint32_t r = 0; r < cgpu::kMaxRegions; ++r) g.reg[r] = ctx->reg[r];
@@ -760,11 +765,19 @@ int cgpu_nat64_4to6(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in, uint8
 // is all or nothing: every mbuf pointer and frame is validated before the
 // first frame is rewritten or the port map changes (a burst of more than one
 // chunk is validated chunk by chunk first).
+// mbufs, or (frames, flen, ftail, out_len) for frame pairs: the device then
+// reads and writes only the frames, and reports out_len for the caller to
+// set data_len / pkt_len.
 static int nat64_mbufs(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, void *const *mbufs, uint32_t n,
-                       uint8_t *disposition, uint8_t *status) {
+                       uint8_t *disposition, uint8_t *status, const uint8_t *const *frames = nullptr,
+                       const uint16_t *flen = nullptr, const uint16_t *ftail = nullptr,
+                       uint16_t *out_len = nullptr) {
   if (!ctx || !pm) return fail(CGPU_EINVAL);
   if (n == 0) return ok();
-  if (!mbufs || !disposition || !status || ctx->nreg == 0) return fail(CGPU_EINVAL);
+  const bool fm = frames != nullptr;
+  if ((!fm && !mbufs) || (fm && (!flen || !out_len || (!to4 && !ftail))) || !disposition ||
+      !status || ctx->nreg == 0)
+    return fail(CGPU_EINVAL);
   DeviceGuard dg(ctx->device);
   if (!dg.ok()) return fail(CGPU_ENODEV);
   const uint32_t m0 = n < kZcChunk ? n : kZcChunk;
@@ -775,23 +788,34 @@ static int nat64_mbufs(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, void *const *m
   const size_t o_ptr = 0, o_off = align_up(8ull * m0, 256), o_len = o_off + align_up(4ull * m0, 256);
   const size_t o_olen = o_len + align_up(2ull * m0, 256), o_disp = o_olen + align_up(2ull * m0, 256);
   const size_t o_st = o_disp + align_up(m0, 256), o_eg = o_st + align_up(m0, 256);
-  const size_t o_cnt = o_eg + align_up(24ull * m0, 256);
+  const size_t o_fl = o_eg + align_up(24ull * m0, 256), o_ft = o_fl + align_up(2ull * m0, 256);
+  const size_t o_cnt = o_ft + align_up(2ull * m0, 256);
   if (int e = grow(&ctx->h_desc, &ctx->d_desc, &ctx->desc_cap, o_cnt + 256)) return fail(e);
   uint8_t *D = ctx->d_desc, *H = ctx->h_desc;
   ZcCounters *dcnt = (ZcCounters *)(D + o_cnt), *hcnt = (ZcCounters *)(H + o_cnt);
   hipStream_t s = ctx->stream;
   const uint32_t slot_extra = to4 ? 0u : 20u;  // 4to6 frames grow by 20 B in their slot
   auto upload = [&](uint32_t at, uint32_t m) {
-    memcpy(H + o_ptr, mbufs + at, 8ull * m);
-    return hipMemcpyAsync(D + o_ptr, H + o_ptr, 8ull * m, hipMemcpyHostToDevice, s) == hipSuccess;
+    if (!fm) {
+      memcpy(H + o_ptr, mbufs + at, 8ull * m);
+      return hipMemcpyAsync(D + o_ptr, H + o_ptr, 8ull * m, hipMemcpyHostToDevice, s) == hipSuccess;
+    }
+    memcpy(H + o_ptr, frames + at, 8ull * m);
+    memcpy(H + o_fl, flen + at, 2ull * m);
+    if (ftail) memcpy(H + o_ft, ftail + at, 2ull * m);
+    return hipMemcpyAsync(D + o_ptr, H + o_ptr, 8ull * m, hipMemcpyHostToDevice, s) == hipSuccess &&
+           hipMemcpyAsync(D + o_fl, H + o_fl, o_cnt - o_fl, hipMemcpyHostToDevice, s) == hipSuccess;
   };
+  const uint64_t *d_frames = fm ? (const uint64_t *)(D + o_ptr) : nullptr;
+  const uint16_t *d_flen = fm ? (const uint16_t *)(D + o_fl) : nullptr;
+  const uint16_t *d_ftail = fm && ftail ? (const uint16_t *)(D + o_ft) : nullptr;
   if (n > m0) {  // validate every chunk before anything is written
     uint32_t bad = 0;
     for (uint32_t at = 0; at < n; at += m0) {
       const uint32_t m = n - at < m0 ? n - at : m0;
       if (!upload(at, m) ||
           gather_chunk(ctx, (const uint64_t *)(D + o_ptr), m, nullptr, 0, nullptr, nullptr, dcnt,
-                       0, nullptr, 0, s) != hipSuccess ||
+                       0, nullptr, 0, s, d_frames, d_flen, d_ftail) != hipSuccess ||
           hipMemcpyAsync(hcnt, dcnt, sizeof(ZcCounters), hipMemcpyDeviceToHost, s) != hipSuccess ||
           hipStreamSynchronize(s) != hipSuccess)
         return fail(CGPU_EIO);
@@ -807,7 +831,7 @@ static int nat64_mbufs(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, void *const *m
       if (!upload(at, m) ||
           gather_chunk(ctx, (const uint64_t *)(D + o_ptr), m, ctx->d_zc, cap,
                        (uint32_t *)(D + o_off), (uint16_t *)(D + o_len), dcnt, slot_extra,
-                       D + o_eg, m0, s) != hipSuccess ||
+                       D + o_eg, m0, s, d_frames, d_flen, d_ftail) != hipSuccess ||
           hipMemcpyAsync(hcnt, dcnt, sizeof(ZcCounters), hipMemcpyDeviceToHost, s) != hipSuccess ||
           hipStreamSynchronize(s) != hipSuccess)
         return fail(CGPU_EIO);
@@ -853,6 +877,13 @@ static int nat64_mbufs(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, void *const *m
       return fail(CGPU_EIO);
     memcpy(disposition + at, H + o_disp, m);
     memcpy(status + at, H + o_st, m);
+    if (fm) {  // out_len of ACT frames (0 otherwise), for the caller's data_len
+      if (hipMemcpyAsync(H + o_olen, D + o_olen, 2ull * m, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+        return fail(CGPU_EIO);
+      const uint16_t *ol = (const uint16_t *)(H + o_olen);
+      for (uint32_t j = 0; j < m; ++j) out_len[at + j] = disposition[at + j] == CGPU_ACT ? ol[j] : 0;
+    }
     at += m;
   }
   return ok();
@@ -862,6 +893,15 @@ int cgpu_nat64_mbufs(cgpu_ctx *ctx, cgpu_portmap *pm, uint32_t direction, void *
                      uint32_t n, uint8_t *disposition, uint8_t *status) {
   if (direction != CGPU_NAT64_6TO4 && direction != CGPU_NAT64_4TO6) return fail(CGPU_EINVAL);
   return nat64_mbufs(direction == CGPU_NAT64_6TO4, ctx, pm, mbufs, n, disposition, status);
+}
+
+int cgpu_nat64_frames(cgpu_ctx *ctx, cgpu_portmap *pm, uint32_t direction,
+                      const uint8_t *const *frames, const uint16_t *len, const uint16_t *tailroom,
+                      uint32_t n, uint16_t *out_len, uint8_t *disposition, uint8_t *status) {
+  if (direction != CGPU_NAT64_6TO4 && direction != CGPU_NAT64_4TO6) return fail(CGPU_EINVAL);
+  if (n != 0 && !frames) return fail(CGPU_EINVAL);
+  return nat64_mbufs(direction == CGPU_NAT64_6TO4, ctx, pm, nullptr, n, disposition, status, frames,
+                     len, tailroom, out_len);
 }
 
 int cgpu_group_by(cgpu_ctx *ctx, const void *key, uint32_t key_kind, uint32_t n,

@@ -127,6 +127,12 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
     const bool ok = valid && (fl == 0u || translate(g, g.frames[i], fl, src));
     if (valid && !ok) atomicAdd(g.bad, 1u);
     L = ok ? fl : 0u;
+    if (valid && g.mb_dev) {  // egress records: the frame only, no header to update
+      g.mb_dev[i] = 0ull;
+      g.fr_dev[i] = ok ? src : 0ull;
+      g.pkt_len[i] = 0u;
+      g.tailroom[i] = g.ftail ? g.ftail[i] : 0u;
+    }
   } else {
     mbuf_frame(g, i, lane, valid, src, L);
   }
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(kBlock) void mbuf_scatter(ScatterArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   bool act = false;
   uint32_t nl = 0;
-  if (i < a.n && a.disposition[i] == CGPU_ACT && a.mb_dev[i] != 0ull) {
+  if (i < a.n && a.disposition[i] == CGPU_ACT && a.fr_dev[i] != 0ull) {
     act = true;
     if (a.delta > 0 && !((uint32_t)a.delta < a.tailroom[i])) {
       act = false;
@@ -201,9 +207,11 @@ __global__ __launch_bounds__(kBlock) void mbuf_scatter(ScatterArgs a) {
       a.status[i] = CGPU_PKT_NOT_RESIZED;
     } else {
       nl = a.out_len[i];
-      uint8_t *h = reinterpret_cast<uint8_t *>(a.mb_dev[i]);
-      *reinterpret_cast<uint16_t *>(h + CGPU_MBUF_DATA_LEN_OFF) = (uint16_t)nl;
-      *reinterpret_cast<uint32_t *>(h + CGPU_MBUF_PKT_LEN_OFF) = a.pkt_len[i] + (uint32_t)a.delta;
+      if (a.mb_dev[i] != 0ull) {  // frame pairs: the caller updates the mbuf
+        uint8_t *h = reinterpret_cast<uint8_t *>(a.mb_dev[i]);
+        *reinterpret_cast<uint16_t *>(h + CGPU_MBUF_DATA_LEN_OFF) = (uint16_t)nl;
+        *reinterpret_cast<uint32_t *>(h + CGPU_MBUF_PKT_LEN_OFF) = a.pkt_len[i] + (uint32_t)a.delta;
+      }
     }
   }
   const uint32_t o = act ? a.out_off[i] : 0u;

@@ -91,6 +91,7 @@ struct GatherArgs {
   const uint64_t *mbufs;  // [n] host rte_mbuf addresses (device copy of the array)
   const uint64_t *frames; // or, when not null: [n] host frame addresses (data_address),
   const uint16_t *flen;   //   [n] their lengths (data_len); no mbuf header is read
+  const uint16_t *ftail;  //   [n] their tailrooms (Mbuf::tailroom), for the egress records
   uint32_t n;
   uint32_t nreg;
   HostRegion reg[kMaxRegions];

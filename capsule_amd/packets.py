@@ -458,6 +458,26 @@ class Nat64Gateway:
         N.check(rc, "cgpu_nat64_mbufs")
         return disp, st
 
+    def nat_frames(self, addrs, lens, tailroom=None, direction="6to4"):
+        """`nat_mbufs` over (data_address, data_len) pairs (u64 / u16 numpy
+        arrays; tailroom u16, needed for 4to6): the device rewrites the
+        frames in place in registered memory and touches no mbuf header.
+        Returns host (out_len, disposition, status); out_len is each ACT
+        frame's new data_len."""
+        addrs = np.ascontiguousarray(addrs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        tr = None if tailroom is None else np.ascontiguousarray(tailroom, dtype=np.uint16)
+        n = len(addrs)
+        olen = np.zeros(n, np.uint16)
+        disp = np.zeros(n, np.uint8)
+        st = np.zeros(n, np.uint8)
+        d = {"6to4": N.NAT64_6TO4, "4to6": N.NAT64_4TO6}[direction]
+        rc = N.lib().cgpu_nat64_frames(self.ctx.handle, self._h, d, addrs.ctypes.data,
+                                       lens.ctypes.data, tr.ctypes.data if tr is not None else None,
+                                       n, olen.ctypes.data, disp.ctypes.data, st.ctypes.data)
+        N.check(rc, "cgpu_nat64_frames")
+        return olen, disp, st
+
     def close(self):
         if self._h:
             N.lib().cgpu_portmap_destroy(self._h)

@@ -348,6 +348,17 @@ int cgpu_nat64_4to6(cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batch *in,
 int cgpu_nat64_mbufs(cgpu_ctx *ctx, cgpu_portmap *pm, uint32_t direction, void *const *mbufs,
                      uint32_t n, uint8_t *disposition, uint8_t *status);
 
+/* The same over a burst handed over as frame pairs: frames[i] / len[i] =
+ * data_address / data_len of mbuf i (mbuf.rs:196-205), tailroom[i] =
+ * buf_len - data_off - data_len (Mbuf::tailroom, mbuf.rs:207-213; needed by
+ * 4to6's extend check, may be NULL for 6to4).  The device reads and writes
+ * only the frames (in registered memory, rewritten in place, every call all
+ * or nothing as above); out_len[i] is the new data_len of each ACT frame (0
+ * otherwise), which the caller stores into data_len / pkt_len.            */
+int cgpu_nat64_frames(cgpu_ctx *ctx, cgpu_portmap *pm, uint32_t direction,
+                      const uint8_t *const *frames, const uint16_t *len, const uint16_t *tailroom,
+                      uint32_t n, uint16_t *out_len, uint8_t *disposition, uint8_t *status);
+
 /* ---- group_by (core/src/batch/group_by.rs:143-172) -----------------------
  * Stable partition of a batch's packet indices by a per-packet arm key: the
  * device form of `batch.group_by(selector, compose!{...})`.  Arm k (k <

@@ -70,6 +70,9 @@ static int (*const p_parse_mbufs)(cgpu_ctx *, void *const *, uint32_t, uint32_t,
 static int (*const p_parse_frames)(cgpu_ctx *, const uint8_t *const *, const uint16_t *, uint32_t,
                                    uint32_t, uint32_t, uint32_t *, uint32_t *, uint64_t *,
                                    cgpu_hdr_record *) = cgpu_parse_frames;
+static int (*const p_nat64_frames)(cgpu_ctx *, cgpu_portmap *, uint32_t, const uint8_t *const *,
+                                   const uint16_t *, const uint16_t *, uint32_t, uint16_t *,
+                                   uint8_t *, uint8_t *) = cgpu_nat64_frames;
 static int (*const p_portmap_create)(cgpu_ctx *, uint32_t, uint16_t,
                                      cgpu_portmap **) = cgpu_portmap_create;
 static void (*const p_portmap_destroy)(cgpu_portmap *) = cgpu_portmap_destroy;
@@ -101,7 +104,7 @@ static const any_fn entry_points[] = {
     (any_fn)p_portmap_next_port, (any_fn)p_portmap_size,  (any_fn)p_nat64_6to4,
     (any_fn)p_nat64_4to6,     (any_fn)p_nat64_mbufs,      (any_fn)p_group_by,
     (any_fn)p_set_ip,         (any_fn)p_last_error,       (any_fn)p_strerror,
-    (any_fn)p_parse_frames,
+    (any_fn)p_parse_frames,   (any_fn)p_nat64_frames,
     (any_fn)p_pkt_status_str, (any_fn)p_abi_version,
 };
 

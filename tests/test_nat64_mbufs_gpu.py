@@ -187,3 +187,63 @@ def test_nat64_mbufs_custom_data_room(ctx):
     finally:
         reg2.close()
         gw.close()
+
+
+def _set_lens(mem, mbufs, olen, disp):
+    """What the caller of cgpu_nat64_frames does: data_len / pkt_len of each
+    ACT mbuf := out_len (the Rust combinator's set of data_len)."""
+    objs = (mbufs - np.uint64(mem.ctypes.data)).astype(np.int64)
+    act = disp == N.ACT
+    v = olen.astype(np.int64)
+    for b, off in ((0, 40), (1, 41)):
+        mem[objs[act] + off] = ((v[act] >> (8 * b)) & 0xFF).astype(np.uint8)
+    for b in range(4):
+        mem[objs[act] + 36 + b] = ((v[act] >> (8 * b)) & 0xFF).astype(np.uint8)
+
+
+def _tailroom(mem, mbufs):
+    objs = (mbufs - np.uint64(mem.ctypes.data)).astype(np.int64)
+    return (_u16(mem, objs + 54) - _u16(mem, objs + 16) - _u16(mem, objs + 40)).astype(np.uint16)
+
+
+@pytest.mark.parametrize("extra", [20, 21])
+def test_nat64_frames_both_directions(ctx, extra):
+    """cgpu_nat64_frames: the same rewrite from (data_address, data_len)
+    pairs; the device touches only the frames, the caller sets data_len from
+    out_len, and then every mbuf matches the oracle as on the mbuf path.  The
+    4to6 replies sit in mbufs with exactly `extra` bytes of room past them."""
+    a, o, l = synth.nat64_stream(20_000, n_keys=3000, drop_frac=0.05, seed=47)
+    mem, mbufs, reg = _pool(ctx, a, o, l, 2048)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=14)
+    pm = oracle_lib.PortMap()
+    try:
+        addrs, lens = synth.mbuf_frames(mem, mbufs)
+        olen_g, disp, st = gw.nat_frames(addrs, lens, direction="6to4")
+        out, olen, odisp, ost = pm.nat_6to4(a, o, l)
+        assert (disp == odisp).all() and (st == ost).all()
+        act = odisp == N.ACT
+        assert (olen_g[act] == olen[act]).all() and (olen_g[~act] == 0).all()
+        objs = (mbufs - np.uint64(mem.ctypes.data)).astype(np.int64)
+        assert (_u16(mem, objs + 40) == l).all()  # no mbuf header written by the device
+        _set_lens(mem, mbufs, olen_g, disp)
+        _check_mbufs(mem, mbufs, a, o, l, out, o, olen, disp)
+        assert gw.next_port() == pm.next_port()
+    finally:
+        reg.close()
+
+    keep = np.nonzero(odisp == N.ACT)[0]
+    ra, ro, rl = synth.nat64_replies(out, o[keep], olen[keep])
+    mem2, mb2, reg2 = _pool(ctx, ra, ro, rl, int(rl.max()) + extra)
+    try:
+        addrs, lens = synth.mbuf_frames(mem2, mb2)
+        tr = _tailroom(mem2, mb2)
+        olen_g, disp6, st6 = gw.nat_frames(addrs, lens, tr, direction="4to6")
+        out6, olen6, odisp6, ost6 = pm.nat_4to6(ra, ro, rl, ro, len(ra))
+        short = tr <= 20
+        assert (disp6[short] == N.ABORT).all() and (st6[short] == N.PKT["NOT_RESIZED"]).all()
+        assert (disp6[~short] == odisp6[~short]).all() and (st6[~short] == ost6[~short]).all()
+        _set_lens(mem2, mb2, olen_g, disp6)
+        _check_mbufs(mem2, mb2, ra, ro, rl, out6, ro, olen6, disp6)
+    finally:
+        reg2.close()
+        gw.close()
