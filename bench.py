@@ -49,35 +49,39 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 INFINITY_CACHE = 256 << 20
 
 
-def make_workload(cfg, seed):
+def _cnt(n):
+    return "1M" if n == 1 << 20 else str(n)
+
+
+def make_workload(cfg, seed, n=1 << 20):
     from capsule_amd import _native as N
     from capsule_amd import synth
 
-    n = 1 << 20
     if cfg == "parse64":
         arena, off, ln = synth.uniform(n, seed=seed)
         flags = N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP | N.F_CSUM_L4 | N.F_FLOW_HASH
-        desc = "1M x 64B Eth/IPv4/UDP: parse + IPv4/UDP checksum verify + 5-tuple hash"
+        desc = f"{_cnt(n)} x 64B Eth/IPv4/UDP: parse + IPv4/UDP checksum verify + 5-tuple hash"
         return dict(arena=arena, off=off, len=ln, flags=flags, kind="parse", desc=desc,
                     algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame="64B")
     if cfg in ("parse256", "parse1500"):  # the metric's other frame sizes, same work as parse64
         size = 256 if cfg == "parse256" else 1500
         arena, off, ln = synth.uniform(n, frame_len=size, seed=seed, slot=(size + 63) // 64 * 64)
         flags = N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP | N.F_CSUM_L4 | N.F_FLOW_HASH
-        desc = f"1M x {size}B Eth/IPv4/UDP: parse + IPv4/UDP checksum verify + 5-tuple hash"
+        desc = f"{_cnt(n)} x {size}B Eth/IPv4/UDP: parse + IPv4/UDP checksum verify + 5-tuple hash"
         return dict(arena=arena, off=off, len=ln, flags=flags, kind="parse", desc=desc,
                     algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame=f"{size}B")
     if cfg == "imix":
-        return imix_header_bytes_workload(seed)
+        return imix_header_bytes_workload(seed, n)
     if cfg == "imix_csum":
         arena, off, ln = synth.imix(n, seed=seed)
         flags = N.F_ACCEPT_ALL | N.F_FLOW_HASH | N.F_CSUM_IP | N.F_CSUM_L4
-        desc = "1M IMIX 64/570/1500 7:4:1 v4/v6 x UDP/TCP: parse + checksums + hash"
+        desc = f"{_cnt(n)} IMIX 64/570/1500 7:4:1 v4/v6 x UDP/TCP: parse + checksums + hash"
         return dict(arena=arena, off=off, len=ln, flags=flags, kind="parse", desc=desc,
-                    algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame="IMIX")
-    if cfg == "nat64":
+                    algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame="IMIX",
+                    line_floor=line_floor_bytes(off, ln))
+    if cfg in ("nat64", "nat64_cold"):
         arena, off, ln = synth.nat64_stream(n, seed=seed)
-        desc = ("1M x 256B IPv6/TCP -> IPv4 6to4 rewrite + TCP/IPv4 checksums (examples/nat64), "
+        desc = (f"{_cnt(n)} x 256B IPv6/TCP -> IPv4 6to4 rewrite + TCP/IPv4 checksums (examples/nat64), "
                 "236-B output frames packed back to back")
         # The egress buffer is packed (a TX ring / DMA-out image): with the
         # frames left in 256-B slots every frame's last output line would be
@@ -85,14 +89,18 @@ def make_workload(cfg, seed):
         new_len = ln.astype(np.int64) - 20
         out_off = np.zeros(n, np.int64)
         out_off[1:] = np.cumsum(new_len)[:-1]
-        return dict(arena=arena, off=off, len=ln, flags=0, kind="nat64", desc=desc,
+        if cfg == "nat64_cold":
+            desc = (f"first pass of the {_cnt(n)} x 256B IPv6/TCP stream over a fresh port map "
+                    "(every key new: ordered NEXT_PORT assignment, main.rs:45-51), 6to4 "
+                    "rewrite + checksums, packed egress")
+        return dict(arena=arena, off=off, len=ln, flags=0, kind=cfg, desc=desc,
                     out_off=out_off.astype(np.uint32), out_size=int(new_len.sum()) + 64,
                     algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame="256B")
     if cfg == "nat64_4to6":
         # the v6 stream that populates the port map; the timed replies are
         # built from its 6to4 output on the device (main())
         arena, off, ln = synth.nat64_stream(n, seed=seed)
-        desc = ("1M x 236B IPv4/TCP replies -> IPv6 4to6 rewrite + TCP checksum "
+        desc = (f"{_cnt(n)} x 236B IPv4/TCP replies -> IPv6 4to6 rewrite + TCP checksum "
                 "(examples/nat64), port map populated by a 6to4 pass")
         return dict(arena=arena, off=off, len=ln, flags=0, kind="nat64_4to6", desc=desc,
                     frame="236B")
@@ -106,7 +114,7 @@ def nat64_4to6_setup(w, ctx, dev):
     from capsule_amd import packets
     from capsule_amd import synth
 
-    gw = packets.Nat64Gateway(ctx, capacity_log2=17)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=PORTMAP_LOG2)
     b = packets.PacketBatch.from_numpy(w["arena"], w["off"], w["len"], dev)
     ob, disp, _ = gw.nat_6to4(b)
     torch.cuda.synchronize(dev)
@@ -118,12 +126,26 @@ def nat64_4to6_setup(w, ctx, dev):
     return gw
 
 
-def imix_header_bytes_workload(seed):
+def line_floor_bytes(off, span):
+    """Bytes of the distinct 128-B lines that [off, off + span) of every
+    packet touches, plus the descriptor arrays (u32 off, u16 len): the HBM
+    read floor of a kernel that reads exactly those bytes, since HBM and L2
+    move whole lines (TCC_EA0_RDREQ_64B ~ 0 on these kernels)."""
+    o = off.astype(np.int64)
+    e = o + np.maximum(span.astype(np.int64), 1) - 1
+    first, last = o >> 7, e >> 7
+    cnt = last - first + 1
+    lines = np.repeat(first, cnt) + (np.arange(int(cnt.sum())) -
+                                     np.repeat(np.cumsum(cnt) - cnt, cnt))
+    n = len(off)
+    return 128 * (len(np.unique(lines)) + -(-4 * n // 128) + -(-2 * n // 128))
+
+
+def imix_header_bytes_workload(seed, n=1 << 20):
     """IMIX parse+hash: algorithmic bytes = headers touched + 6 B descriptor."""
     from capsule_amd import _native as N
     from capsule_amd import synth
 
-    n = 1 << 20
     arena, off, ln = synth.imix(n, seed=seed)
     eth = np.full(n, 14, np.int64)
     l3 = np.zeros(n, np.int64)
@@ -138,8 +160,8 @@ def imix_header_bytes_workload(seed):
     algo = int((eth + l3 + l4 + 6).sum())
     flags = N.F_ACCEPT_ALL | N.F_FLOW_HASH
     return dict(arena=arena, off=off, len=ln, flags=flags, kind="parse", frame="IMIX",
-                desc="1M IMIX 64/570/1500 7:4:1 v4/v6 x UDP/TCP: parse + 5-tuple hash",
-                algo_bytes=algo)
+                desc=f"{_cnt(n)} IMIX 64/570/1500 7:4:1 v4/v6 x UDP/TCP: parse + 5-tuple hash",
+                algo_bytes=algo, line_floor=line_floor_bytes(off, eth + l3 + l4))
 
 
 def cpu_baseline(w, seconds):
@@ -173,6 +195,13 @@ def cpu_baseline(w, seconds):
         if w["kind"] == "nat64_4to6":
             pm.nat_6to4(*w["setup"])  # same port map as the device side
             fn = L.or_nat64_4to6
+        if w["kind"] == "nat64_cold":  # every pass over a fresh map (the map's
+            # construction is inside the sample, as the device's reset is not)
+            def cold():
+                m = oracle_lib.PortMap()
+                return fn(m.h, p(arena), p(off), p(ln), n, p(out), p(off), p(olen), p(disp),
+                          p(st))
+            return cold
         return lambda: (pm, fn(pm.h, p(arena), p(off), p(ln), n, p(out), p(off),
                                p(olen), p(disp), p(st)))
 
@@ -251,12 +280,12 @@ def cpu_baseline(w, seconds):
 
 
 SEEDS = {"parse64": 2, "parse256": 2, "parse1500": 2, "imix": 3, "imix_csum": 3, "nat64": 4,
-         "nat64_4to6": 4}
+         "nat64_4to6": 4, "nat64_cold": 4}
 CONFIGS = tuple(SEEDS)
 METRIC = "Mpps device-resident parse+cksum+hash @64/256/1500B; % HBM-read roofline"
 # the metric's other sizes and BASELINE's other single-GPU configs, timed in
 # the same N=1 run (the `sizes` object of the line)
-SIZES = ("parse256", "parse1500", "imix", "imix_csum", "nat64")
+SIZES = ("parse256", "parse1500", "imix", "imix_csum", "nat64", "nat64_4to6", "nat64_cold")
 # BASELINE config 5: IMIX shards, one per GPU (the `shards` object)
 SHARD_CONFIG = "imix"
 MIN_WARM_S = 0.15  # device time of warm-up before any timed region (steady clocks)
@@ -278,7 +307,7 @@ def pmc_traffic(cfg):
     return None
 
 
-def bench_config(cfg, g, ctx, dev, steps, warmup, w=None, queues=1):
+def bench_config(cfg, g, ctx, dev, steps, warmup, w=None, queues=1, n_pkts=1 << 20):
     """Time one config on this rank.
 
     Builds the rank's shard of the workload, keeps R copies resident in HBM
@@ -297,8 +326,10 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None, queues=1):
 
     from capsule_amd import packets
 
-    w = w or make_workload(cfg, g.shard_seed(0xC0FFEE + SEEDS[cfg]))
+    w = w or make_workload(cfg, g.shard_seed(0xC0FFEE + SEEDS[cfg]), n=n_pkts)
     n = len(w["off"])
+    if w["kind"] == "nat64_cold":
+        return bench_nat64_cold(cfg, g, ctx, dev, steps, warmup, w)
     gw = nat64_4to6_setup(w, ctx, dev) if w["kind"] == "nat64_4to6" else None
     batch_bytes = len(w["arena"]) + 6 * n
     copies = max(2, -(-2 * INFINITY_CACHE // batch_bytes))
@@ -383,7 +414,8 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None, queues=1):
         kern_us = elapsed / steps * 1e6
     res = dict(cfg=cfg, n=n, desc=w["desc"], frame=w["frame"], copies=copies, elapsed=elapsed, queues=queues,
                steps=steps, kern_us=kern_us, algo_bytes=w["algo_bytes"],
-               achieved=w["algo_bytes"] / (kern_us * 1e-6) / 1e9, w=w)
+               achieved=w["algo_bytes"] / (kern_us * 1e-6) / 1e9, w=w,
+               line_floor=w.get("line_floor"))
     del launchers, outs, batches, b0
     if gw is not None:
         gw.close()
@@ -392,13 +424,19 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None, queues=1):
     return res
 
 
+# per-rank device identity (ordinal, PCI address), gathered once in main():
+# a scaling line then shows which GPU each rank's figures come from
+DEVICES = [None]
+
+
 def summarize(r, g):
     """Aggregate of one config over the ranks (collective: every rank calls
     it in the same order)."""
     fr = g.gather(r["achieved"] / HBM_PEAK_GBS)
     us = g.gather(r["kern_us"])
     total = g.sum(r["n"] * r["steps"])
-    return {
+    devs = DEVICES if len(DEVICES) == len(us) else [None] * len(us)
+    s = {
         "workload": r["desc"], "packets_per_step": r["n"], "steps": r["steps"],
         "mpps": round(total / r["elapsed"] / 1e6, 2),
         "ms_per_step": round(r["elapsed"] / r["steps"] * 1e3, 5),
@@ -407,9 +445,95 @@ def summarize(r, g):
         "frac": round(r["achieved"] / HBM_PEAK_GBS, 4),
         "algo_bytes_per_launch": r["algo_bytes"],
         "traffic": r["traffic"] if "traffic" in r else pmc_traffic(r["cfg"]),
-        "per_rank": [{"rank": i, "kernel_us": round(u, 3), "frac": round(f, 4)}
-                     for i, (u, f) in enumerate(zip(us, fr))],
+        "per_rank": [{"rank": i, "kernel_us": round(u, 3), "frac": round(f, 4), "device": d}
+                     for i, (u, f, d) in enumerate(zip(us, fr, devs))],
     }
+    if r.get("line_floor"):
+        # HBM and L2 move 128-B lines: the bytes of the distinct lines the
+        # kernel must touch in this layout, and the fraction of the peak the
+        # kernel reaches on them
+        lf = r["line_floor"]
+        s["line_floor_bytes"] = lf
+        s["frac_of_line_floor"] = round(lf / (r["kern_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+    for k in ("note",):
+        if r.get(k):
+            s[k] = r[k]
+    return s
+
+
+def device_identity(ordinal):
+    import torch
+
+    p = torch.cuda.get_device_properties(ordinal)
+    return {"ordinal": ordinal, "name": p.name,
+            "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"}
+
+
+def check_devices(devs, one_device):
+    """Each rank on its own GPU (distinct PCI addresses), unless the N-rank
+    path is being rehearsed on one card (CGPU_BENCH_ONE_DEVICE=1)."""
+    pcis = [d["pci"] for d in devs]
+    if not one_device and len(set(pcis)) != len(pcis):
+        raise SystemExit(f"bench.py: ranks share a GPU ({pcis}); set CGPU_BENCH_ONE_DEVICE=1 "
+                         "to rehearse N ranks on one device")
+
+
+def bench_nat64_cold(cfg, g, ctx, dev, steps, warmup, w):
+    """The cold port map: every timed call is the first pass of the stream
+    over a freshly reset map (cgpu_portmap_reset, enqueued on the stream
+    before the call), so every key is new and its port comes from the
+    ordered NEXT_PORT assignment (assigned_port's miss path, main.rs:45-51:
+    the fused kernel defers every frame, the tail kernel orders the keys and
+    rewrites them).  kernel_us = device time of the call alone (HIP events
+    after the reset and after the tail); the wall-clock rate includes the
+    resets."""
+    import torch
+
+    from capsule_amd import packets
+
+    n = len(w["off"])
+    stream = torch.cuda.current_stream(dev)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=PORTMAP_LOG2)
+    b = packets.PacketBatch.from_numpy(w["arena"], w["off"], w["len"], dev)
+    oo = torch.from_numpy(w["out_off"].view(np.int32)).to(dev)
+    out = (torch.empty(w["out_size"], dtype=torch.uint8, device=dev), oo,
+           torch.empty(n, dtype=torch.int16, device=dev),
+           torch.empty(n, dtype=torch.uint8, device=dev),
+           torch.empty(n, dtype=torch.uint8, device=dev))
+    launch = packets.Nat64Launcher(gw, b, out, stream, "6to4")
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    for a, z in evs:  # create the HIP events outside the timed region
+        a.record(stream)
+        z.record(stream)
+    for _ in range(max(3, min(warmup, 20))):
+        gw.reset(stream=stream)
+        launch()
+    torch.cuda.synchronize(dev)
+    keys = gw.size()  # every call starts over: the map holds exactly one pass's keys
+    assert 0 < keys <= n and gw.next_port() == (1025 + keys) & 0xFFFF, "cold pass"
+    state = {"j": 0}
+
+    def one():
+        j = state["j"]
+        gw.reset(stream=stream)
+        evs[j][0].record(stream)
+        launch()
+        evs[j][1].record(stream)
+        state["j"] = j + 1
+
+    elapsed = g.timed(one, steps, sync=lambda: torch.cuda.synchronize(dev))
+    kern_us = sum(a.elapsed_time(z) for a, z in evs) / steps * 1e3
+    keys = gw.size()
+    gw.close()
+    del launch, out, b
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    return dict(cfg=cfg, n=n, desc=w["desc"], frame=w["frame"], copies=1, elapsed=elapsed,
+                queues=1, steps=steps, kern_us=kern_us, algo_bytes=w["algo_bytes"],
+                achieved=w["algo_bytes"] / (kern_us * 1e-6) / 1e9, w=w,
+                note=f"{keys} new keys per call; mpps and ms_per_step include the map reset "
+                     "before each call, kernel_us and frac do not")
 
 
 def stub_worker(args):
@@ -419,12 +543,17 @@ def stub_worker(args):
     from capsule_amd.shards import ShardGroup
 
     g = ShardGroup()
+    same = os.environ.get("CGPU_BENCH_STUB_SAME_DEVICE") == "1"  # (test of check_devices)
+    DEVICES[:] = g.gather_obj({"ordinal": g.local_rank, "name": "stub",
+                               "pci": "stub:00" if same else f"stub:{g.local_rank:02x}"})
+    check_devices(DEVICES, os.environ.get("CGPU_BENCH_ONE_DEVICE") == "1")
 
     def fake(cfg, steps):
         el = g.timed(lambda: time.sleep(1e-4 * (1 + g.rank)), steps)
         return dict(cfg=cfg, n=1 << 20, desc=f"stub {cfg}", frame="-", copies=0, elapsed=el,
                     steps=steps, kern_us=100.0 * (1 + g.rank), algo_bytes=70 << 20,
-                    achieved=(70 << 20) / (1e-4 * (1 + g.rank)) / 1e9, w=None, traffic=None)
+                    achieved=(70 << 20) / (1e-4 * (1 + g.rank)) / 1e9, w=None, traffic=None,
+                    line_floor=(108 << 20) if cfg.startswith("imix") else None)
 
     main = fake(args.config, args.steps)
     extra = {} if args.only else {"shards": dict(summarize(fake(SHARD_CONFIG, args.steps), g),
@@ -491,6 +620,9 @@ def main():
                     help="time the --config only (no `shards` / `sizes` objects; for profiling)")
     ap.add_argument("--sub-steps", type=int, default=300,
                     help="timed launches of each `shards` / `sizes` config (at least --steps)")
+    ap.add_argument("--n", type=int, default=1 << 20,
+                    help="packets per batch (default 1 Mi, the BASELINE configs; smaller for "
+                         "the bench-mode tests)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--e2e", action="store_true",
                     help="host-resident batches: pinned H2D + parse + D2H, pipelined (DESIGN.md §8)")
@@ -526,18 +658,21 @@ def main():
     g = ShardGroup()
     # CGPU_BENCH_ONE_DEVICE=1: every rank on GPU 0 (rehearsing the N-rank
     # path on a one-GPU box; the ranks then share the card)
-    ordinal = 0 if os.environ.get("CGPU_BENCH_ONE_DEVICE") == "1" else g.local_rank
+    one_device = os.environ.get("CGPU_BENCH_ONE_DEVICE") == "1"
+    ordinal = 0 if one_device else g.local_rank
     dev = torch.device("cuda", ordinal)
     torch.cuda.set_device(dev)
+    DEVICES[:] = g.gather_obj(device_identity(ordinal))
+    check_devices(DEVICES, one_device)
     ctx = packets.Context(ordinal)
 
-    main_r = bench_config(args.config, g, ctx, dev, args.steps, args.warmup)
+    main_r = bench_config(args.config, g, ctx, dev, args.steps, args.warmup, n_pkts=args.n)
     extra = {}
     if not args.only:
         sub = max(args.steps, args.sub_steps)
         # BASELINE config 5: this rank's IMIX shard, all ranks at once
         shard_r = (main_r if args.config == SHARD_CONFIG else
-                   bench_config(SHARD_CONFIG, g, ctx, dev, sub, args.warmup))
+                   bench_config(SHARD_CONFIG, g, ctx, dev, sub, args.warmup, n_pkts=args.n))
         extra["shards"] = dict(summarize(shard_r, g), config=SHARD_CONFIG,
                                roofline_basis="header bytes the reference touches + 6-B "
                                               "descriptor (SURVEY.md §8d)")
@@ -545,7 +680,7 @@ def main():
             sizes = {}
             for c in SIZES:
                 r = shard_r if c == SHARD_CONFIG else bench_config(c, g, ctx, dev, sub,
-                                                                     args.warmup)
+                                                                     args.warmup, n_pkts=args.n)
                 sizes[c] = summarize(r, g)
                 if r is not shard_r:
                     r["w"] = None
@@ -556,7 +691,8 @@ def main():
             # streams, launches alternating): the chip's rate when launches
             # overlap instead of draining one by one (context for `value`,
             # which stays one queue per GPU)
-            q = bench_config(args.config, g, ctx, dev, sub, args.warmup, w=main_r["w"], queues=2)
+            q = bench_config(args.config, g, ctx, dev, sub, args.warmup, w=main_r["w"], queues=2,
+                             n_pkts=args.n)
             extra["rx_queues"] = {
                 "queues": 2, "mpps": round(q["n"] * q["steps"] / q["elapsed"] / 1e6, 2),
                 "us_per_launch_wall": round(q["kern_us"], 3),
@@ -590,7 +726,7 @@ def bench_nat64_mbufs(args, w):
     mem, mbufs = synth.mbuf_pool(w["arena"], w["off"], w["len"], mem=pinned.numpy(), room=room)
     orig = mem.copy()
     reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
-    gw = packets.Nat64Gateway(ctx, capacity_log2=17)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=PORTMAP_LOG2)
     B = min(args.burst, n)
     bursts = [mbufs[s:s + B] for s in range(0, n - B + 1, B)]
     frames = args.ingress == "frames"
@@ -640,7 +776,7 @@ def e2e_mbufs(args):
     from capsule_amd import packets, synth
 
     torch.cuda.set_device(0)
-    w = make_workload(args.config, 0xC0FFEE + 2)
+    w = make_workload(args.config, 0xC0FFEE + 2, n=args.n)
     if w["kind"] == "nat64" and args.config == "nat64" and args.ingress in ("zero_copy", "frames"):
         return bench_nat64_mbufs(args, w)
     if w["kind"] != "parse":
@@ -710,9 +846,11 @@ def e2e(args):
 
     from capsule_amd import packets
 
+    if args.config == "nat64_cold":
+        raise SystemExit("--e2e: nat64_cold is a device-resident timing of the map's first pass")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    w = make_workload(args.config, 0xC0FFEE + 2)
+    w = make_workload(args.config, 0xC0FFEE + 2, n=args.n)
     n = len(w["off"])
     ctx = packets.Context(0)
     gw = nat64_4to6_setup(w, ctx, dev) if w["kind"] == "nat64_4to6" else None
@@ -735,9 +873,8 @@ def e2e(args):
             host_out[d][1].copy_(outs[d].flow_hash, non_blocking=True)
         down_bytes = 12 * n
     else:
-        assert queues == 1, "one port map, one queue"
         direction = "4to6" if gw is not None else "6to4"
-        gw = gw or packets.Nat64Gateway(ctx, capacity_log2=17)
+        gw = gw or packets.Nat64Gateway(ctx, capacity_log2=PORTMAP_LOG2)
         nat = [(torch.empty_like(bufs[d].arena), bufs[d].off,
                 torch.empty(n, dtype=torch.int16, device=dev),
                 torch.empty(n, dtype=torch.uint8, device=dev),

@@ -14,7 +14,7 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ.get("CAPSULE_GPU_LIB", _HERE / "libcapsule_gpu.so"))
 
 # ---- constants (include/capsule_gpu.h) ------------------------------------
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OK, EINVAL, ENOMEM, ENODEV, EIO, ENOSPC = 0, -22, -12, -19, -5, -28
 
@@ -127,7 +127,7 @@ EXPORTS = [
     "cgpu_portmap_size", "cgpu_nat64_6to4", "cgpu_nat64_4to6", "cgpu_group_by", "cgpu_last_error", "cgpu_strerror",
     "cgpu_pkt_status_str", "cgpu_abi_version", "cgpu_host_register", "cgpu_host_unregister",
     "cgpu_parse_mbufs", "cgpu_set_ip", "cgpu_nat64_mbufs", "cgpu_parse_frames",
-    "cgpu_nat64_frames",
+    "cgpu_nat64_frames", "cgpu_portmap_reset",
 ]
 
 _lib = None
@@ -167,6 +167,8 @@ def lib():
     L.cgpu_portmap_next_port.argtypes = [vp, P(u16)]
     L.cgpu_portmap_size.restype = i32
     L.cgpu_portmap_size.argtypes = [vp, P(u32)]
+    L.cgpu_portmap_reset.restype = i32
+    L.cgpu_portmap_reset.argtypes = [vp, u16, vp]
     L.cgpu_nat64_6to4.restype = i32
     L.cgpu_nat64_6to4.argtypes = [vp, vp, P(Batch), vp, ctypes.c_uint64, vp, vp, vp, vp, vp]
     L.cgpu_nat64_4to6.restype = i32

@@ -88,10 +88,14 @@ struct cgpu_portmap {
   void *rec_b = nullptr;
   uint32_t scratch_n = 0;
   uint32_t calls = 0;  // 6to4 calls: parity of the deferred-list counter
-  // the stream of the latest call: calls on one map are stream-ordered
-  // (the map is stateful), so draining it drains the map's work without
-  // stalling other contexts' streams on the same GPU
-  hipStream_t last = nullptr;
+  // recorded on the stream of every call that uses the map: calls on one
+  // map are stream-ordered (the map is stateful), so waiting for it waits
+  // for the map's work without stalling other contexts' streams on the same
+  // GPU, and it stays valid after the caller destroys that stream
+  hipEvent_t done = nullptr;
+  // the stream of the latest call (compared, never used: it may be gone);
+  // a call on another stream first waits for `done`
+  void *last_stream = nullptr;
   uint32_t room = 2048u;  // Nat64Args::room of the next call (65535 inside cgpu_nat64_mbufs)
 };
 
@@ -619,6 +623,13 @@ int cgpu_parse_mbufs(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32_t fla
   return parse_staged(ctx, n, get, flags, meta, csum, flow_hash, fields);
 }
 
+// The hot index (kernels.hpp HotBucket): 2^hot_log2 buckets of three
+// entries, a quarter of the slots up to 2^15 buckets (2 MiB, room for the
+// 65536 gateway ports' worth of keys at half load).
+#ifndef CGPU_HOT_LOG2_MAX
+#define CGPU_HOT_LOG2_MAX 15
+#endif
+
 int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_port,
                         cgpu_portmap **out) {
   if (!ctx || !out || capacity_log2 < 4 || capacity_log2 > 29) return fail(CGPU_EINVAL);
@@ -626,7 +637,11 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
   DeviceGuard dg(ctx->device);
   if (!dg.ok()) return fail(CGPU_ENODEV);
   const size_t cap = (size_t)1 << capacity_log2;
-  const size_t bytes = 256 + 65536 * 8 + cap * sizeof(cgpu::PortSlot);
+  const uint32_t hot_log2 = capacity_log2 - 2 < CGPU_HOT_LOG2_MAX ? capacity_log2 - 2 : CGPU_HOT_LOG2_MAX;
+  const size_t hot = (size_t)1 << hot_log2;
+  const size_t o_rev = 256, o_hot = o_rev + 65536 * sizeof(cgpu::RevEntry);
+  const size_t o_slots = o_hot + hot * sizeof(cgpu::HotBucket);
+  const size_t bytes = o_slots + cap * sizeof(cgpu::PortSlot);
   void *mem = nullptr;
   if (hipMalloc(&mem, bytes) != hipSuccess) return fail(CGPU_ENOMEM);
   cgpu_portmap *pm = new (std::nothrow) cgpu_portmap();
@@ -636,14 +651,23 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
   }
   pm->ctx = ctx;
   pm->mem = mem;
-  pm->last = ctx->stream;
   uint8_t *p = (uint8_t *)mem;
   pm->dev.state = (uint32_t *)p;
-  pm->dev.rev = (uint64_t *)(p + 256);
-  pm->dev.slots = (cgpu::PortSlot *)(p + 256 + 65536 * 8);
+  pm->dev.rev = (cgpu::RevEntry *)(p + o_rev);
+  pm->dev.hot = (cgpu::HotBucket *)(p + o_hot);
+  pm->dev.slots = (cgpu::PortSlot *)(p + o_slots);
   pm->dev.cap_mask = (uint32_t)(cap - 1);
+  pm->dev.hot_mask = (uint32_t)(hot - 1);
+  pm->dev.hot_shift = 32u - hot_log2;
+  if (hipEventCreateWithFlags(&pm->done, hipEventDisableTiming) != hipSuccess) {
+    (void)hipFree(mem);
+    delete pm;
+    return fail(CGPU_EIO);
+  }
   if (cgpu::launch_portmap_init(pm->dev, first_port, ctx->stream) != hipSuccess ||
+      hipEventRecord(pm->done, ctx->stream) != hipSuccess ||
       hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    (void)hipEventDestroy(pm->done);
     (void)hipFree(mem);
     delete pm;
     return fail(CGPU_EIO);
@@ -652,10 +676,24 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
   return ok();
 }
 
+int cgpu_portmap_reset(cgpu_portmap *pm, uint16_t first_port, void *stream) {
+  if (!pm) return fail(CGPU_EINVAL);
+  DeviceGuard dg(pm->ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
+  // behind the map's earlier calls, whatever stream they ran on
+  if (hipStreamWaitEvent((hipStream_t)stream, pm->done, 0) != hipSuccess) return fail(CGPU_EIO);
+  hipError_t e = cgpu::launch_portmap_init(pm->dev, first_port, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e);
+  if (hipEventRecord(pm->done, (hipStream_t)stream) != hipSuccess) return fail(CGPU_EIO);
+  pm->last_stream = stream;
+  return ok();
+}
+
 void cgpu_portmap_destroy(cgpu_portmap *pm) {
   if (!pm) return;
   DeviceGuard dg(pm->ctx->device);
-  (void)hipStreamSynchronize(pm->last);
+  (void)hipEventSynchronize(pm->done);
+  (void)hipEventDestroy(pm->done);
   if (pm->pkt_slot) (void)hipFree(pm->pkt_slot);
   (void)hipFree(pm->mem);
   delete pm;
@@ -664,9 +702,10 @@ void cgpu_portmap_destroy(cgpu_portmap *pm) {
 static int read_state(cgpu_portmap *pm, uint32_t st[4]) {
   DeviceGuard dg(pm->ctx->device);
   if (!dg.ok()) return CGPU_ENODEV;
-  // behind the map's latest call, on its own stream
-  if (hipMemcpyAsync(st, pm->dev.state, 16, hipMemcpyDeviceToHost, pm->last) != hipSuccess ||
-      hipStreamSynchronize(pm->last) != hipSuccess)
+  // behind the map's latest call (its event), then on the context's stream
+  if (hipEventSynchronize(pm->done) != hipSuccess ||
+      hipMemcpyAsync(st, pm->dev.state, 16, hipMemcpyDeviceToHost, pm->ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(pm->ctx->stream) != hipSuccess)
     return CGPU_EIO;
   return 0;
 }
@@ -738,11 +777,15 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   a.par = pm->calls & 1u;
   a.room = pm->room;
   a.pm = pm->dev;
+  if (stream != pm->last_stream &&
+      hipStreamWaitEvent((hipStream_t)stream, pm->done, 0) != hipSuccess)
+    return fail(CGPU_EIO);
+  pm->last_stream = stream;
   hipError_t e = to4 ? cgpu::launch_nat64_6to4(a, (hipStream_t)stream)
                      : cgpu::launch_nat64_4to6(a, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e);
   if (to4) ++pm->calls;
-  pm->last = (hipStream_t)stream;
+  if (hipEventRecord(pm->done, (hipStream_t)stream) != hipSuccess) return fail(CGPU_EIO);
   return ok();
 }
 

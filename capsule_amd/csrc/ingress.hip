@@ -17,7 +17,8 @@
 // flight before any store.  Every host address is translated through the
 // registered regions and range-checked first: a pointer outside them, or a
 // frame that runs past its own buffer, is counted (the call fails) and never
-// dereferenced.  No slot is written past the arena's capacity.
+// dereferenced; for nat64 egress the check covers every byte the rewritten
+// frame may occupy.  No slot is written past the arena's capacity.
 #include "capsule_gpu.h"
 #include "device_common.hpp"
 #include "kernels.hpp"
@@ -102,7 +103,10 @@ __device__ __forceinline__ void mbuf_frame(const GatherArgs &g, uint32_t i, uint
     // invariant of every mbuf Mbuf::extend / shrink maintain) and in a
     // registered region
     const uint64_t buf_addr = ((uint64_t)ba_hi << 32) | ba_lo;
-    ok = doff + dlen <= blen && (dlen == 0u || translate(g, buf_addr + doff, dlen, src));
+    // with the bytes a 4to6 rewrite may grow into (extend's tailroom check)
+    const uint32_t tail = (blen - doff - dlen) & 0xffffu;
+    const uint32_t span = dlen + (g.slot_extra != 0u && tail > g.slot_extra ? g.slot_extra : 0u);
+    ok = doff + dlen <= blen && (dlen == 0u || translate(g, buf_addr + doff, span, src));
     L = ok ? dlen : 0u;
     if (!ok) atomicAdd(g.bad, 1u);
   }
@@ -124,7 +128,11 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
     // (data_address, data_len) pairs from the RX core: the frame alone, one
     // request per 64 B of frame, no mbuf header line
     const uint32_t fl = valid ? g.flen[i] : 0u;
-    const bool ok = valid && (fl == 0u || translate(g, g.frames[i], fl, src));
+    // the bytes the egress may write too: a 4to6 frame grows by slot_extra
+    // when its tailroom allows (the scatter's extend check)
+    const uint32_t ft = valid && g.ftail ? g.ftail[i] : 0u;
+    const uint32_t span = fl + (g.slot_extra != 0u && ft > g.slot_extra ? g.slot_extra : 0u);
+    const bool ok = valid && (fl == 0u || translate(g, g.frames[i], span, src));
     if (valid && !ok) atomicAdd(g.bad, 1u);
     L = ok ? fl : 0u;
     if (valid && g.mb_dev) {  // egress records: the frame only, no header to update

@@ -22,8 +22,9 @@
 //     at the shifted position;
 //   - DPP quad broadcasts give every lane the header dwords; each lane
 //     classifies by the reference control flow (Act / Drop / Abort);
-//   - lane 0 looks the key up in the device port map (6to4: open-addressing
-//     PORT_MAP; 4to6: the ADDR_MAP reverse array, read by the whole quad);
+//   - lane 0 looks the key up in the device port map (6to4: the hot index,
+//     then the open-addressing PORT_MAP; 4to6: the ADDR_MAP array, one 32-B
+//     value per gateway port, read by the whole quad);
 //   - each lane patches its chunks in registers and sums its part of the TCP
 //     span with v_sad_u16; the quad reduces; the lane holding the TCP
 //     checksum field stores it last.
@@ -288,6 +289,100 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, rsrc_t rs,
   return kNoSlot;
 }
 
+// ---- the hot index (kernels.hpp HotBucket) ------------------------------------
+// A committed key is found in one 64-B bucket (rarely the next ones, when an
+// insert found its bucket full): its header dword, then the one entry whose
+// fingerprint matches.  A miss is final once a bucket has not overflowed:
+// the key was never inserted past it.  Every miss falls back to the
+// authoritative table, so the index only ever short-cuts a lookup whose
+// answer is fixed (a committed key's port never changes).
+constexpr uint32_t kHotFull = 4u;  // bucket count value: full, overflowed
+
+__device__ __forceinline__ uint32_t hot_bucket(const PortMapDev &pm, uint32_t hraw) {
+  return (hraw * 0x9e3779b1u) >> pm.hot_shift;
+}
+
+__device__ __forceinline__ uint32_t hot_fp(uint32_t hraw) {
+  return ((hraw * 0x85ebca6bu) >> 11) & 0xffu;
+}
+
+// Bucket b with header dword w0: true and the port if the key is there;
+// `more` when the bucket overflowed (look in the next one).
+__device__ __forceinline__ bool hot_in_bucket(const PortMapDev &pm, uint32_t b, uint32_t w0,
+                                              const uint32_t (&key)[5], uint32_t fp,
+                                              uint32_t &port, bool &more) {
+  const uint32_t cnt = w0 & 0xffu;
+  more = cnt > kHotWays;
+  for (uint32_t j = 0; j < kHotWays && j < cnt; ++j) {
+    if (((w0 >> (8u + 8u * j)) & 0xffu) != fp) continue;
+    const uint32_t *e = pm.hot[b].w + 1u + 5u * j;
+    const u32x4 k4 = *reinterpret_cast<const u32x4 *>(e);  // dword-aligned
+    const uint32_t k5 = e[4];
+    if (k4[0] == key[0] && k4[1] == key[1] && k4[2] == key[2] && k4[3] == key[3] &&
+        (k5 & 0xffffu) == key[4]) {
+      port = k5 >> 16;
+      return true;
+    }
+  }
+  return false;
+}
+
+// The whole lookup, given the first bucket's header dword.
+__device__ __forceinline__ bool hot_find(const PortMapDev &pm, const uint32_t (&key)[5], uint32_t hraw,
+                                         uint32_t w0, uint32_t &port) {
+  const uint32_t fp = hot_fp(hraw);
+  uint32_t b = hot_bucket(pm, hraw);
+  for (uint32_t t = 0;;) {
+    bool more;
+    if (hot_in_bucket(pm, b, w0, key, fp, port, more)) return true;
+    if (!more || ++t == kHotProbes) return false;
+    b = (b + 1u) & pm.hot_mask;
+    w0 = pm.hot[b].w[0];
+  }
+}
+
+// Insert a key just committed with its port (the tail kernel; lookups of it
+// start with the next call).  An entry is claimed by a CAS on the bucket's
+// header (count + 1, the key's fingerprint); a full bucket is marked
+// overflowed and the key tries the next; after kHotProbes buckets the key
+// stays in the authoritative table only.
+__device__ __forceinline__ void hot_insert(const PortMapDev &pm, const uint32_t (&key)[5],
+                                           uint32_t port) {
+  const uint32_t hraw = key_hash(key), fp = hot_fp(hraw);
+  uint32_t b = hot_bucket(pm, hraw);
+  for (uint32_t t = 0; t < kHotProbes; ++t) {
+    uint32_t *hw = &pm.hot[b].w[0];
+    uint32_t old = __hip_atomic_load(hw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), c;
+    for (;;) {
+      c = old & 0xffu;
+      if (c >= kHotFull) break;
+      const uint32_t nw = c < kHotWays ? old + 1u + (fp << (8u + 8u * c)) : old + 1u;
+      const uint32_t prev = atomicCAS(hw, old, nw);
+      if (prev == old) break;
+      old = prev;
+    }
+    if (c < kHotWays) {
+      uint32_t *e = pm.hot[b].w + 1u + 5u * c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) e[j] = key[j];
+      e[4] = key[4] | (port << 16);
+      return;
+    }
+    b = (b + 1u) & pm.hot_mask;
+  }
+}
+
+// assigned_port (main.rs:41-53) lookup for frame i with the key's hash: the
+// hot index first, then the authoritative table (probe_port_at).
+__device__ __forceinline__ uint32_t probe_port_key(const Nat64Args &a, rsrc_t rs, uint32_t i,
+                                                   const uint32_t (&key)[5], uint32_t hraw,
+                                                   uint32_t &port) {
+  if (hot_find(a.pm, key, hraw, a.pm.hot[hot_bucket(a.pm, hraw)].w[0], port)) return 0u;
+  const uint32_t h = hraw & a.pm.cap_mask;
+  const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
+  return probe_port_at(a, rs, i, key, h, sp[0], sp[1], port);
+}
+
 // assigned_port (main.rs:41-53) lookup for frame i: returns the table slot
 // (kNoSlot: table full) and, for a key committed by an earlier batch, its
 // port; a key first seen in this batch is claimed (CAS) or joined, and its
@@ -296,9 +391,7 @@ __device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, rsrc_t rs, ui
                                                uint32_t &port) {
   uint32_t key[5];
   make_key(v, key);
-  const uint32_t h = key_hash(key) & a.pm.cap_mask;
-  const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
-  return probe_port_at(a, rs, i, key, h, sp[0], sp[1], port);
+  return probe_port_key(a, rs, i, key, key_hash(key), port);
 }
 
 // ---- the rewrite of one frame by its quad (fused kernels and K5) -------------
@@ -967,14 +1060,10 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   const bool act0 = valid && v.disp == CGPU_ACT;
   uint32_t key[5];
   make_key(v, key);
-  const uint32_t h = key_hash(key) & a.pm.cap_mask;
-  u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
+  const uint32_t hraw = key_hash(key);
+  uint32_t hw0 = 0u;
 #ifndef CGPU_NAT64_ABL_NOPROBE
-  if (act0) {
-    const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
-    s0 = sp[0];
-    s1 = sp[1];
-  }
+  if (act0) hw0 = a.pm.hot[hot_bucket(a.pm, hraw)].w[0];  // the key's hot bucket header, examined after B1
 #endif
   const uint32_t nl = len - 20u;  // meaningful for ACT frames
   if (mine) {
@@ -994,7 +1083,15 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     slot = 0u;
     port = 1025u;
 #else
-    slot = probe_port_at(a, rs, i, key, h, s0, s1, port);
+    // the hot index; on a miss (a key new in this batch, or one the index
+    // has no room for) the authoritative table
+    if (hot_find(a.pm, key, hraw, hw0, port)) {
+      slot = 0u;
+    } else {
+      const uint32_t h = hraw & a.pm.cap_mask;
+      const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
+      slot = probe_port_at(a, rs, i, key, h, sp[0], sp[1], port);
+    }
 #endif
   }
   if (v.disp == CGPU_ACT && slot == kNoSlot) {
@@ -1141,14 +1238,27 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_tail(Nat64Args a, uint
         const uint32_t slot = ps & kSlotMask;
         const uint32_t ordinal = pre + below;
         const uint32_t port = (a.pm.state[0] + ordinal) & 0xffffu;  // NEXT_PORT.fetch_add order
+        uint32_t key[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) key[j] = a.pm.slots[slot].w[1 + j];
         // ADDR_MAP.insert_new(port, key) (main.rs:50): the first mapping of a
-        // port wins, also after NEXT_PORT wraps; ordinals are global
-        const uint64_t tag = ((uint64_t)(a.pm.state[1] + ordinal) << 32) | slot;
-        atomicMin((unsigned long long *)&a.pm.rev[port], (unsigned long long)tag);
-        // PORT_MAP.insert_new (main.rs:49): commit the key for later batches
+        // port wins, also after NEXT_PORT wraps.  This call's ordinals o and
+        // o + 65536k share a port, so only its first lap (o < 65536) can be
+        // first, and only if no earlier call mapped the port: one writer per
+        // entry, no race.
+        if (ordinal < 65536u) {
+          RevEntry &e = a.pm.rev[port];
+          if (!(e.w[4] & kRevValid)) {
+            *reinterpret_cast<u32x4 *>(&e.w[0]) = u32x4{key[0], key[1], key[2], key[3]};
+            e.w[4] = key[4] | kRevValid;
+          }
+        }
+        // PORT_MAP.insert_new (main.rs:49): commit the key for later batches,
+        // and copy it into the hot index
         a.pm.slots[slot].w[7] = 0xffffffffu;
         a.pm.slots[slot].w[0] = kPersist;
         __hip_atomic_store(&a.pm.slots[slot].w[6], port, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        hot_insert(a.pm, key, port);
       }
       // 2. the chunk's deferred frames: compact them, a quad per frame
       const bool d = ps != kNoSlot;
@@ -1200,8 +1310,8 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_tail(Nat64Args a, uint
 }
 
 // ============================ 4to6 direction =================================
-// Classify, look the TCP destination port up in the reverse map ADDR_MAP
-// (rev[port] -> slot -> the v6 key), build the IPv6 header, then the quad
+// Classify, look the TCP destination port up in ADDR_MAP (rev[port] = the
+// v6 key itself, one 32-B read), build the IPv6 header, then the quad
 // rewrite with the input shifted by -20 bytes behind the 40-byte header (the
 // TCP checksum field, output bytes 70+4k, is in chunk 4).
 // 4to6 classification of one frame (main.rs:86-118) up to the ADDR_MAP
@@ -1261,20 +1371,19 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_4to6_fused(Nat64Args a
   gather_header(Y, Y4, P);
   V4 v;
   classify4(P, d.len, v);
-  // assigned_addr(port) (main.rs:56-58): ADDR_MAP as the reverse array; the
-  // quad's lanes read the same words (one request per quad)
+  // assigned_addr(port) (main.rs:56-58): ADDR_MAP holds the value, one 32-B
+  // entry per gateway port; the quad's lanes read the same words (one
+  // request per quad)
   u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
   if (d.valid && v.disp == CGPU_ACT) {
-    const uint64_t r = a.pm.rev[v.gw_port];
-    if (r == ~0ull) {
+    const u32x4 *rp = reinterpret_cast<const u32x4 *>(&a.pm.rev[v.gw_port]);
+    s0 = rp[0];
+    s1 = rp[1];
+    if (!(s1[0] & kRevValid)) {
       v.disp = CGPU_DROP;  // no mapping: Either::Drop
     } else if (d.len >= a.room - 20u) {  // push::<Ipv6>(): extend 40 needs 40 < tailroom
       v.st = CGPU_PKT_NOT_RESIZED;
       v.disp = CGPU_ABORT;
-    } else {
-      const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[(uint32_t)r]);
-      s0 = sp[0];
-      s1 = sp[1];
     }
   }
   const bool act = d.valid && v.disp == CGPU_ACT;
@@ -1300,27 +1409,35 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_4to6_fused(Nat64Args a
   f.V[4] = 0u;
   f.V[5] = v.L[3];       // v4 source address
   // V6..V9: the ADDR_MAP key, the original v6 source
-  f.V[6] = s0[1];
-  f.V[7] = s0[2];
-  f.V[8] = s0[3];
-  f.V[9] = s1[0];
+  f.V[6] = s0[0];
+  f.V[7] = s0[1];
+  f.V[8] = s0[2];
+  f.V[9] = s0[3];
   uint32_t ph = 0;       // v6 pseudo-header addresses, LE residue
   ph = sad16(f.V[2], ph);
   ph = sad16(f.V[5], ph);
-  ph = sad16(s0[1], sad16(s0[2], sad16(s0[3], sad16(s1[0], ph))));
+  ph = sad16(s0[0], sad16(s0[1], sad16(s0[2], sad16(s0[3], ph))));
   f.ph = fold32(ph);
-  f.info = v.k | kNow | (s1[1] << 16);  // the original v6-side port
+  f.info = v.k | kNow | ((s1[0] & 0xffffu) << 16);  // the original v6-side port
   rewrite_quad<false>(a, rs, ors, g, d, al16, f, X, E);
 }
 
 __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i <= pm.cap_mask) {
-#pragma unroll
-    for (int j = 0; j < 7; ++j) pm.slots[i].w[j] = 0u;
-    pm.slots[i].w[7] = 0xffffffffu;
+    u32x4 *s = reinterpret_cast<u32x4 *>(&pm.slots[i]);
+    s[0] = u32x4{0u, 0u, 0u, 0u};
+    s[1] = u32x4{0u, 0u, 0u, 0xffffffffu};
   }
-  if (i < 65536u) pm.rev[i] = ~0ull;
+  if (i < 65536u) {
+    u32x4 *r = reinterpret_cast<u32x4 *>(&pm.rev[i]);
+    r[0] = r[1] = u32x4{0u, 0u, 0u, 0u};
+  }
+  if (i <= pm.hot_mask) {
+    u32x4 *h = reinterpret_cast<u32x4 *>(&pm.hot[i]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) h[c] = u32x4{0u, 0u, 0u, 0u};
+  }
   if (i == 0) {
     pm.state[0] = first_port;
     pm.state[1] = 0u;
@@ -1346,6 +1463,7 @@ uint32_t nat64_num_blocks(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 constexpr uint32_t kTailGrid = CGPU_NAT64_TAIL_GRID;  // workgroups of K2 / K5
 
 hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStream_t s) {
+  // one thread per slot, ADDR_MAP entry and hot-index bucket
   const uint32_t cap = pm.cap_mask + 1u > 65536u ? pm.cap_mask + 1u : 65536u;
   hipLaunchKernelGGL(portmap_init, dim3((cap + 255) / 256), dim3(256), 0, s, pm, first_port);
   return hipGetLastError();

@@ -405,6 +405,11 @@ class Nat64Gateway:
         N.check(N.lib().cgpu_portmap_size(self._h, ctypes.byref(v)), "size")
         return v.value
 
+    def reset(self, first_port=1025, stream=None):
+        """Empty the map (as a fresh gateway), asynchronously on `stream`."""
+        N.check(N.lib().cgpu_portmap_reset(self._h, first_port, _stream_handle(stream)),
+                "cgpu_portmap_reset")
+
     def _call(self, fn, what, grow, batch, out_arena, out_off, stream, out):
         n = batch.n
         dev = batch.arena.device

@@ -85,6 +85,17 @@ class ShardGroup:
         dist.all_gather(out, torch.tensor([float(value)], dtype=torch.float64))
         return [float(t.item()) for t in out]
 
+    def gather_obj(self, value):
+        """[value of rank 0, value of rank 1, ...] on every rank (any picklable
+        value: the per-rank device identities of the bench line)."""
+        if not self.pg:
+            return [value]
+        import torch.distributed as dist
+
+        out = [None] * self.world
+        dist.all_gather_object(out, value)
+        return out
+
     def timed(self, fn, steps, sync=None):
         """sync + barrier, run `steps` calls of fn, sync; returns the max over
         ranks of the elapsed seconds (each rank's clock stops at its own

@@ -32,7 +32,14 @@
 extern "C" {
 #endif
 
-#define CGPU_ABI_VERSION 2
+/* ABI history:
+ *   2  round-2 layout.
+ *   3  cgpu_portmap_reset; CGPU_MAX_BATCH is 2^30 - 1; group_by's
+ *      CGPU_KEY_META_CLASS sends ICMP to the catch-all arm (4); mbufs with
+ *      data_off + data_len > buf_len are rejected (CGPU_EINVAL); the mbuf
+ *      and frame-pair entry points also check that every byte a frame may
+ *      be rewritten into lies in a registered region.                     */
+#define CGPU_ABI_VERSION 3
 
 /* ---- call-level return codes (negative errno style) -------------------- */
 #define CGPU_OK 0
@@ -298,9 +305,16 @@ typedef struct cgpu_portmap cgpu_portmap;
 int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_port,
                         cgpu_portmap **out);
 void cgpu_portmap_destroy(cgpu_portmap *pm);
-/* Synchronous reads of the map state (test/debug helpers).               */
+/* Synchronous reads of the map state (test/debug helpers).  They wait for
+ * the map's latest call by an event the library records on that call's
+ * stream, so the caller may destroy the stream first.                     */
 int cgpu_portmap_next_port(cgpu_portmap *pm, uint16_t *next_port);
 int cgpu_portmap_size(cgpu_portmap *pm, uint32_t *entries);
+/* Empty the map again (PORT_MAP, ADDR_MAP, NEXT_PORT = first_port), as a
+ * fresh cgpu_portmap_create would leave it, asynchronously on `stream`
+ * behind the map's earlier calls.  Calls on one map are ordered: a call on
+ * another stream than the previous one waits for it.                      */
+int cgpu_portmap_reset(cgpu_portmap *pm, uint16_t first_port, void *stream);
 
 /* Disposition per packet (reference batch/mod.rs:54-107, filter_map.rs:73):
  * ACT = Either::Keep (emitted), DROP = Either::Drop, ABORT = Err.          */

@@ -78,6 +78,7 @@ static int (*const p_portmap_create)(cgpu_ctx *, uint32_t, uint16_t,
 static void (*const p_portmap_destroy)(cgpu_portmap *) = cgpu_portmap_destroy;
 static int (*const p_portmap_next_port)(cgpu_portmap *, uint16_t *) = cgpu_portmap_next_port;
 static int (*const p_portmap_size)(cgpu_portmap *, uint32_t *) = cgpu_portmap_size;
+static int (*const p_portmap_reset)(cgpu_portmap *, uint16_t, void *) = cgpu_portmap_reset;
 static int (*const p_nat64_6to4)(cgpu_ctx *, cgpu_portmap *, const cgpu_batch *, uint8_t *,
                                  uint64_t, const uint32_t *, uint16_t *, uint8_t *, uint8_t *,
                                  void *) = cgpu_nat64_6to4;
@@ -105,7 +106,7 @@ static const any_fn entry_points[] = {
     (any_fn)p_nat64_4to6,     (any_fn)p_nat64_mbufs,      (any_fn)p_group_by,
     (any_fn)p_set_ip,         (any_fn)p_last_error,       (any_fn)p_strerror,
     (any_fn)p_parse_frames,   (any_fn)p_nat64_frames,
-    (any_fn)p_pkt_status_str, (any_fn)p_abi_version,
+    (any_fn)p_pkt_status_str, (any_fn)p_abi_version,    (any_fn)p_portmap_reset,
 };
 
 int main(void) {

@@ -85,16 +85,19 @@ def _gpu_nat(gw, direction, arena, off, ln, out_off, size):
 
 
 def test_bench_nat64_config_every_byte(ctx):
-    """BASELINE config 4 exactly as benched: the 1 M x 256-B stream, first
-    pass (every key new) and the steady-state pass the timed loop repeats
-    (every key known); all output bytes, lengths, dispositions and the port
-    map state equal the oracle's.  Then the replies through 4to6 (the
-    nat64_4to6 bench config)."""
+    """BASELINE config 4 exactly as benched: the 1 M x 256-B stream through
+    a map of the bench's capacity (bench.PORTMAP_LOG2), first pass (every
+    key new: the nat64_cold config) and the steady-state pass the timed loop
+    repeats (every key known, looked up through the hot index); all output
+    bytes, lengths, dispositions and the port map state equal the oracle's.
+    Then a cold pass again after cgpu_portmap_reset (how nat64_cold times
+    it), and the replies through 4to6 (the nat64_4to6 bench config)."""
+    import bench
     from capsule_amd import packets
 
     w = _workload("nat64")
     a, o, l = w["arena"], w["off"], w["len"]
-    gw = packets.Nat64Gateway(ctx, capacity_log2=17)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=bench.PORTMAP_LOG2)
     pm = oracle_lib.PortMap()
     oo, size = w["out_off"], w["out_size"]  # the bench's packed egress layout
     for p in range(2):
@@ -103,6 +106,10 @@ def test_bench_nat64_config_every_byte(ctx):
         _compare_nat(g, ref, f"6to4 pass {p}")
         assert (ref[2] == N.ACT).all()
         assert gw.next_port() == pm.next_port() and gw.size() == pm.size()
+    gw.reset()
+    _compare_nat(_gpu_nat(gw, "6to4", a, o, l, oo, size), oracle_lib.PortMap().nat_6to4(a, o, l, oo, size),
+                 "6to4 after reset")
+    assert gw.next_port() == pm.next_port() and gw.size() == pm.size()
     ra, ro, rl = synth.nat64_replies(ref[0], oo, ref[1])
     o6 = (np.arange(len(ro), dtype=np.int64) * 256).astype(np.uint32)  # +20 B per frame
     g = _gpu_nat(gw, "4to6", ra, ro, rl, o6, 256 * len(ro) + 64)

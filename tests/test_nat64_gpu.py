@@ -115,7 +115,7 @@ def test_config4_full_size_properties(ctx):
     n, keys = 1 << 20, 50_000
     a, o, l = synth.nat64_stream(n, n_keys=keys)
     b = packets.PacketBatch.from_numpy(a, o, l, DEV)
-    gw = packets.Nat64Gateway(ctx, capacity_log2=17)
+    gw = packets.Nat64Gateway(ctx)  # the library default, 2^20 slots (the bench's)
     ob, disp, st = gw.nat_6to4(b)
     r = packets.parse(ctx, ob, flags=N.F_ACCEPT_ALL | N.F_CSUM_IP | N.F_CSUM_L4, fields=True)
     torch.cuda.synchronize()
@@ -240,3 +240,79 @@ def test_4to6_round_trip_properties(ctx):
         assert int(rec["dst_port"][j]) == int.from_bytes(bytes(sport[j]), "big")
         k = {0x8100: 1, 0x88A8: 2}.get(int.from_bytes(fr[12:14], "big"), 0)
         assert bytes(rec["src_ip"][j]) == bytes.fromhex("0064ff9b0000000000000000") + fr[26 + 4 * k : 30 + 4 * k]
+
+
+def _nat_both(ctx, gw, pm, direction, arena, off, ln, out_off, size):
+    """One call on the GPU gateway and the oracle: every output byte, length,
+    disposition and status compared; returns the oracle's outputs."""
+    from capsule_amd import packets
+
+    out_arena = torch.zeros(size, dtype=torch.uint8, device=DEV)
+    oo = torch.from_numpy(np.ascontiguousarray(out_off, np.uint32).view(np.int32)).to(DEV)
+    b = packets.PacketBatch.from_numpy(arena, off, ln, DEV)
+    fn = gw.nat_6to4 if direction == "6to4" else gw.nat_4to6
+    ob, disp, st = fn(b, out_arena=out_arena, out_off=oo)
+    torch.cuda.synchronize()
+    ref = (pm.nat_6to4 if direction == "6to4" else pm.nat_4to6)(arena, off, ln, out_off, size)
+    got = (out_arena.cpu().numpy(), ob.len.cpu().numpy().view(np.uint16), disp.cpu().numpy(),
+           st.cpu().numpy())
+    for name, x, y in zip(("output arena", "length", "disposition", "status"), got, ref):
+        bad = np.nonzero(x != y)[0]
+        assert not len(bad), f"{direction}: {name} differs at {bad[:8]}"
+    return ref
+
+
+def test_hot_index_overflow_falls_back(ctx):
+    """A map whose hot index (kernels.hpp HotBucket) is far too small for its
+    keys (16 buckets of three entries for 30 keys), so buckets overflow,
+    lookups walk overflow chains and some keys are found only in the
+    authoritative table; then 200 keys in a 128-bucket index.  Ports, frames and the replies through 4to6 still
+    equal the oracle's over several batches."""
+    from capsule_amd import packets
+
+    gw = packets.Nat64Gateway(ctx, capacity_log2=6)  # 64 slots, 2^(6-2) = 16 hot buckets
+    pm = oracle_lib.PortMap()
+    a, o, l = synth.nat64_stream(3000, n_keys=30, seed=52, drop_frac=0.05)
+    for _ in range(3):  # first pass: keys new; then every lookup through the index
+        out, olen, disp, _ = _nat_both(ctx, gw, pm, "6to4", a, o, l, o, len(a) + 64)
+    keep = np.nonzero(disp == N.ACT)[0]
+    ra, ro, rl = synth.nat64_replies(out, o[keep], olen[keep])
+    o6 = (np.arange(len(ro), dtype=np.int64) * 256).astype(np.uint32)
+    _nat_both(ctx, gw, pm, "4to6", ra, ro, rl, o6, 256 * len(ro) + 64)
+    gw.close()
+    # 200 keys in a 128-bucket index (384 entries, at most 4 buckets probed)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=9)
+    pm = oracle_lib.PortMap()
+    a, o, l = synth.nat64_stream(6000, n_keys=200, seed=53)
+    for _ in range(3):
+        _nat_both(ctx, gw, pm, "6to4", a, o, l, o, len(a) + 64)
+    assert gw.size() == pm.size() and gw.next_port() == pm.next_port()
+    gw.close()
+
+
+def test_addr_map_first_mapping_wins(ctx):
+    """ADDR_MAP.insert_new (main.rs:50): when NEXT_PORT wraps, a port keeps
+    its first key.  Batch 1 brings more than 65536 new keys (the port
+    sequence wraps inside one call); batch 2 brings more, whose ports were
+    already mapped.  4to6 replies to every frame of both batches must go
+    where the oracle sends them."""
+    from capsule_amd import packets
+
+    gw = packets.Nat64Gateway(ctx, capacity_log2=18)
+    pm = oracle_lib.PortMap()
+    n, cut = 160_000, 120_000
+    a, o, l = synth.nat64_stream(n, n_keys=100_000, seed=51)
+    outs = []
+    for s, e in ((0, cut), (cut, n)):
+        base = int(o[s])
+        aa, oo, ll = a[base:int(o[e - 1]) + 256], o[s:e] - np.uint32(base), l[s:e]
+        out, olen, disp, _ = _nat_both(ctx, gw, pm, "6to4", aa, oo, ll, oo, len(aa) + 64)
+        outs.append((out, oo, olen, disp))
+    assert pm.size() > 65536 + 10_000 and gw.size() == pm.size()
+    for out, oo, olen, disp in outs:
+        keep = np.nonzero(disp == N.ACT)[0]
+        ra, ro, rl = synth.nat64_replies(out, oo[keep], olen[keep])
+        o6 = (np.arange(len(ro), dtype=np.int64) * 256).astype(np.uint32)
+        ref = _nat_both(ctx, gw, pm, "4to6", ra, ro, rl, o6, 256 * len(ro) + 64)
+        assert (ref[2] == N.ACT).all()
+    gw.close()

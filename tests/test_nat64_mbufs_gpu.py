@@ -247,3 +247,42 @@ def test_nat64_frames_both_directions(ctx, extra):
     finally:
         reg2.close()
         gw.close()
+
+
+def test_nat64_egress_range_checked(ctx):
+    """The bytes a 4to6 rewrite may grow into are range-checked with the
+    frame: a frame that ends 10 B before its registered region does, but
+    whose tailroom says 20 more bytes fit, fails the call (frame pairs with a
+    caller-supplied tailroom, and rte_mbufs whose buf_len claims the room)
+    before anything is written.  With that frame's true tailroom the call
+    goes through, and that frame is NotResized."""
+    a, o, l = synth.nat64_stream(512, n_keys=64, seed=48)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=12)
+    pm = oracle_lib.PortMap()
+    gw.nat_6to4(packets.PacketBatch.from_numpy(a, o, l, "cuda:0"))
+    out, olen, odisp, _ = pm.nat_6to4(a, o, l)
+    keep = np.nonzero(odisp == N.ACT)[0]
+    ra, ro, rl = synth.nat64_replies(out, o[keep], olen[keep])
+    mem, mbufs = synth.mbuf_pool(ra, ro, rl, room=2048)
+    addrs, lens = synth.mbuf_frames(mem, mbufs)
+    top = int(np.argmax(addrs))
+    end = int(addrs[top]) + int(lens[top]) + 10 - mem.ctypes.data
+    reg = packets.HostRegion(ctx, mem.ctypes.data, end)
+    before = mem.copy()
+    try:
+        tr = np.full(len(addrs), 100, np.uint16)
+        with pytest.raises(N.CgpuError) as e:
+            gw.nat_frames(addrs, lens, tr, direction="4to6")
+        assert e.value.code == N.EINVAL and (mem == before).all()
+        with pytest.raises(N.CgpuError) as e:
+            gw.nat_mbufs(mbufs, "4to6")
+        assert e.value.code == N.EINVAL and (mem == before).all()
+        tr[top] = 10
+        olen_g, disp, st = gw.nat_frames(addrs, lens, tr, direction="4to6")
+        assert disp[top] == N.ABORT and st[top] == N.PKT["NOT_RESIZED"]
+        rest = np.arange(len(addrs)) != top
+        assert (disp[rest] == N.ACT).all()
+        assert (mem[end - 10:end] == before[end - 10:end]).all()
+    finally:
+        reg.close()
+        gw.close()

@@ -118,7 +118,11 @@ def test_bench_single_gpu_line_shape():
     for k in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "dtype",
               "config", "roofline"):
         assert k in d
-    assert set(d["sizes"]) == {"parse256", "parse1500", "imix", "imix_csum", "nat64"}
+    assert set(d["sizes"]) == {"parse256", "parse1500", "imix", "imix_csum", "nat64",
+                               "nat64_4to6", "nat64_cold"}
+    for obj in (d["shards"], d["sizes"]["imix"], d["sizes"]["imix_csum"]):
+        assert obj["line_floor_bytes"] > 0 and 0 < obj["frac_of_line_floor"]
+    assert d["roofline"]["per_rank"][0]["device"]["pci"] == "stub:00"
     assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(d["roofline"])
     assert "unpinned" in d["parity"]["flow_hash"]
 
@@ -129,3 +133,33 @@ def test_shard_group_refuses_device_backend():
 
     with pytest.raises(ValueError):
         ShardGroup(backend="nccl")
+
+
+def test_bench_eight_ranks_stub():
+    """The driver's 8-GPU line shape: 8 rank processes, one row per rank with
+    its own device (distinct PCI addresses), n_gpus 8."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--stub", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=600,
+                       env=_stub_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _bench_line(r.stdout)
+    assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 8 * d["config"]["packets_per_step"]
+    rows = d["roofline"]["per_rank"]
+    assert [x["rank"] for x in rows] == list(range(8))
+    assert len({x["device"]["pci"] for x in rows}) == 8
+    assert len(d["shards"]["per_rank"]) == 8
+
+
+def test_bench_refuses_shared_device_stub():
+    """Ranks that report the same PCI address fail the run unless the
+    one-device rehearsal is asked for."""
+    env = dict(_stub_env(), CGPU_BENCH_STUB_SAME_DEVICE="1")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--stub", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=300,
+                       env=env, cwd=ROOT)
+    assert r.returncode != 0 and "share a GPU" in r.stderr
+    env["CGPU_BENCH_ONE_DEVICE"] = "1"
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--stub", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=300,
+                       env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
