@@ -84,8 +84,6 @@ struct cgpu_portmap {
   // per-call scratch
   uint32_t *pkt_slot = nullptr;
   uint64_t *lookback = nullptr;
-  void *rec_h = nullptr;  // deferred frames' header records
-  void *rec_b = nullptr;
   uint32_t scratch_n = 0;
   uint32_t calls = 0;  // 6to4 calls: parity of the deferred-list counter
   // recorded on the stream of every call that uses the map: calls on one
@@ -744,17 +742,13 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
     const size_t nb = cgpu::nat64_num_blocks(in->n) + 1;
     void *m = nullptr;
     const size_t o_sums = align_up(4ull * in->n, 256);
-    const size_t o_rech = o_sums + align_up(8ull * nb, 256);
-    const size_t o_recb = o_rech + align_up(16ull * in->n, 256);
-    const size_t o_end = o_recb + align_up(8ull * in->n, 256);
+    const size_t o_end = o_sums + align_up(8ull * nb, 256);
     if (hipMalloc(&m, o_end + 256) != hipSuccess) return fail(CGPU_ENOMEM);
     pm->pkt_slot = (uint32_t *)m;
     pm->lookback = (uint64_t *)((uint8_t *)m + o_sums);
     // status 0 = "not published" in every epoch
     if (hipMemsetAsync(pm->lookback, 0, 8ull * nb, (hipStream_t)stream) != hipSuccess)
       return fail(CGPU_EIO);
-    pm->rec_h = (uint8_t *)m + o_rech;
-    pm->rec_b = (uint8_t *)m + o_recb;
     pm->scratch_n = in->n;
   }
   cgpu::Nat64Args a;
@@ -772,8 +766,6 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   a.pkt_slot = pm->pkt_slot;
   a.lookback = pm->lookback;
   a.epoch = pm->calls;
-  a.rec_h = (cgpu::u32x4 *)pm->rec_h;
-  a.rec_b = (uint2 *)pm->rec_b;
   a.par = pm->calls & 1u;
   a.room = pm->room;
   a.pm = pm->dev;

@@ -97,10 +97,8 @@ struct Nat64Args {
   uint8_t *disposition;
   uint8_t *status;
   uint32_t *pkt_slot;    // scratch [n]: table slot (or 0xffffffff)
-  uint64_t *lookback;    // scratch [nblocks]: K2's decoupled look-back words
+  uint64_t *lookback;    // scratch [nblocks]: the tail's decoupled look-back words
   uint32_t epoch;        // 6to4 call number (look-back words of other calls are stale)
-  u32x4 *rec_h;          // scratch [n]: deferred 6to4 frames' IPv4 header dwords 0..3
-  uint2 *rec_b;          // scratch [n]: header dword 4, VLAN depth
   uint32_t par;          // call parity: selects the per-call counters state[4/6/9 + par]
   uint32_t room;         // data room of Mbuf::extend's tailroom model (mbuf.rs:225-233):
                          // 2048 for device batches; 65535 on the mbuf path, whose

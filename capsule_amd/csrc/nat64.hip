@@ -237,7 +237,7 @@ __device__ __forceinline__ void ipv4_header(const V6 &v, uint32_t len, uint32_t 
 // assigned_port (main.rs:41-53) lookup for frame i: returns the table slot
 // (kNoSlot: table full) and, for a key committed by an earlier batch, its
 // port; a key first seen in this batch is claimed (CAS) or joined, and its
-// first packet index recorded (atomicMin) for K2..K4.
+// first packet index recorded (atomicMin) for the tail kernel.
 __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, rsrc_t rs, uint32_t i,
                                                   const uint32_t (&key)[5], uint32_t h, u32x4 s0,
                                                   u32x4 s1, uint32_t &port) {
@@ -307,14 +307,21 @@ __device__ __forceinline__ uint32_t hot_fp(uint32_t hraw) {
 }
 
 // Bucket b with header dword w0: true and the port if the key is there;
-// `more` when the bucket overflowed (look in the next one).
+// `more` when the bucket overflowed (look in the next one).  Only entries
+// whose fingerprint matches are read: one read for almost every lookup (a
+// false match costs a second), so a wave waits for one round trip.
 __device__ __forceinline__ bool hot_in_bucket(const PortMapDev &pm, uint32_t b, uint32_t w0,
                                               const uint32_t (&key)[5], uint32_t fp,
                                               uint32_t &port, bool &more) {
   const uint32_t cnt = w0 & 0xffu;
   more = cnt > kHotWays;
-  for (uint32_t j = 0; j < kHotWays && j < cnt; ++j) {
-    if (((w0 >> (8u + 8u * j)) & 0xffu) != fp) continue;
+  uint32_t cand = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kHotWays; ++j)
+    if (j < cnt && ((w0 >> (8u + 8u * j)) & 0xffu) == fp) cand |= 1u << j;
+  while (cand) {
+    const uint32_t j = __builtin_ctz(cand);
+    cand &= cand - 1u;
     const uint32_t *e = pm.hot[b].w + 1u + 5u * j;
     const u32x4 k4 = *reinterpret_cast<const u32x4 *>(e);  // dword-aligned
     const uint32_t k5 = e[4];
@@ -374,10 +381,14 @@ __device__ __forceinline__ void hot_insert(const PortMapDev &pm, const uint32_t 
 
 // assigned_port (main.rs:41-53) lookup for frame i with the key's hash: the
 // hot index first, then the authoritative table (probe_port_at).
+// (CGPU_NAT64_NO_HOT: A/B build without the hot-index lookups; the tail
+// still fills the index.)
 __device__ __forceinline__ uint32_t probe_port_key(const Nat64Args &a, rsrc_t rs, uint32_t i,
                                                    const uint32_t (&key)[5], uint32_t hraw,
                                                    uint32_t &port) {
+#ifndef CGPU_NAT64_NO_HOT
   if (hot_find(a.pm, key, hraw, a.pm.hot[hot_bucket(a.pm, hraw)].w[0], port)) return 0u;
+#endif
   const uint32_t h = hraw & a.pm.cap_mask;
   const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
   return probe_port_at(a, rs, i, key, h, sp[0], sp[1], port);
@@ -386,7 +397,7 @@ __device__ __forceinline__ uint32_t probe_port_key(const Nat64Args &a, rsrc_t rs
 // assigned_port (main.rs:41-53) lookup for frame i: returns the table slot
 // (kNoSlot: table full) and, for a key committed by an earlier batch, its
 // port; a key first seen in this batch is claimed (CAS) or joined, and its
-// first packet index recorded (atomicMin) for K2..K4.
+// first packet index recorded (atomicMin) for the tail kernel.
 __device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, rsrc_t rs, uint32_t i, const V6 &v,
                                                uint32_t &port) {
   uint32_t key[5];
@@ -394,7 +405,7 @@ __device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, rsrc_t rs, ui
   return probe_port_key(a, rs, i, key, key_hash(key), port);
 }
 
-// ---- the rewrite of one frame by its quad (fused kernels and K5) -------------
+// ---- the rewrite of one frame by its quad (the fused kernel's quad path) -----
 // A frame record: info = k | kNow | port << 16 (6to4: the assigned port;
 // 4to6: the original v6-side port); V = the new IP header as LE dwords (6to4:
 // IPv4 H[0..4]; 4to6: the 40-B IPv6 header); ph = 4to6 pseudo-header residue.
@@ -572,26 +583,6 @@ __device__ __forceinline__ void rewrite_frame(const Nat64Args &a, rsrc_t rs, rsr
     for (uint32_t j = 0; j < kFJ; ++j) chunk_out<TO4, FAST>(a, ors, f, 16u * q + kFG * j + g, o[j], acc, held);
   }
   finish_frame<TO4, FAST>(a, ors, f, g, acc, held);
-}
-
-// Runs rewrite_frame with the wave-uniform FAST decision (K5's frames).
-template <bool TO4>
-__device__ __forceinline__ bool wave_fast(const Nat64Args &a, bool act, const FrameRec &f) {
-  return !__ballot(act && !((f.in_off & 3u) == 0u && (f.o_off & 3u) == 0u &&
-                            (uint64_t)f.in_off + f.new_len + 64u <= (uint64_t)a.arena_len &&
-                            (uint64_t)f.o_off + f.new_len + 16u <= (uint64_t)a.out_arena_len));
-}
-
-template <bool TO4>
-__device__ __forceinline__ void rewrite_dispatch(const Nat64Args &a, rsrc_t rs, rsrc_t ors,
-                                                 uint32_t g, const FrameRec &f, bool act) {
-  const u32x4 none[kFJ] = {};
-  if (wave_fast<TO4>(a, act, f)) {
-    if (act) rewrite_frame<TO4, true, false>(a, rs, ors, g, f, true, none);
-  } else {
-    const bool in_al_wave = !__ballot(act && (f.in_off & 3u) != 0u);
-    if (act) rewrite_frame<TO4, false, false>(a, rs, ors, g, f, in_al_wave, none);
-  }
 }
 
 // ---- fused kernels: one 4-lane quad per frame -----------------------------
@@ -836,26 +827,22 @@ __device__ __forceinline__ void quad_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   const bool act = d.valid && v.disp == CGPU_ACT;
   uint32_t H[5];
   ipv4_header(v, d.len, H);
-  const bool now = act && port != 0xffffffffu;  // committed key: finished here
-  const bool deferred = act && !now;            // new key: its port needs the batch order (K2..K5)
+  const bool now = act && port != 0xffffffffu;  // committed key: its port is known
+  const bool deferred = act && !now;            // new key: its port needs the batch order (tail)
   if (d.valid && g == 0u) {
-    if (deferred) {
-      a.rec_h[d.i] = u32x4{H[0], H[1], H[2], H[3]};
-      a.rec_b[d.i] = make_uint2(H[4], v.k);
-    }
-    a.out_len[d.i] = now ? (uint16_t)d.nl : 0;
+    a.out_len[d.i] = act ? (uint16_t)d.nl : 0;
     a.pkt_slot[d.i] = now ? kNoSlot : slot;
     a.disposition[d.i] = (uint8_t)v.disp;
     a.status[d.i] = (uint8_t)v.st;
   }
   defer_append(a, lane, deferred && g == 0u, d.i);
 #ifndef CGPU_NAT64_ABL_NOREWRITE  // timing ablation only: classify + probe alone
-  if (now) {
+  if (act) {  // a deferred frame is written with source port 0; the tail patches it
     FrameRec f;
     f.in_off = d.off;
     f.o_off = d.o_off;
     f.new_len = d.nl;
-    f.info = v.k | kNow | (port << 16);
+    f.info = v.k | kNow | ((now ? port : 0u) << 16);
 #pragma unroll
     for (int j = 0; j < 5; ++j) f.V[j] = H[j];
 #pragma unroll
@@ -1062,7 +1049,14 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   make_key(v, key);
   const uint32_t hraw = key_hash(key);
   uint32_t hw0 = 0u;
-#ifndef CGPU_NAT64_ABL_NOPROBE
+#if defined(CGPU_NAT64_NO_HOT)
+  u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
+  if (act0) {
+    const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[hraw & a.pm.cap_mask]);
+    s0 = sp[0];
+    s1 = sp[1];
+  }
+#elif !defined(CGPU_NAT64_ABL_NOPROBE)
   if (act0) hw0 = a.pm.hot[hot_bucket(a.pm, hraw)].w[0];  // the key's hot bucket header, examined after B1
 #endif
   const uint32_t nl = len - 20u;  // meaningful for ACT frames
@@ -1085,6 +1079,10 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
 #else
     // the hot index; on a miss (a key new in this batch, or one the index
     // has no room for) the authoritative table
+#ifdef CGPU_NAT64_NO_HOT
+    (void)hw0;
+    slot = probe_port_at(a, rs, i, key, hraw & a.pm.cap_mask, s0, s1, port);
+#else
     if (hot_find(a.pm, key, hraw, hw0, port)) {
       slot = 0u;
     } else {
@@ -1092,6 +1090,7 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
       const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
       slot = probe_port_at(a, rs, i, key, h, sp[0], sp[1], port);
     }
+#endif
 #endif
   }
   if (v.disp == CGPU_ACT && slot == kNoSlot) {
@@ -1106,20 +1105,18 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   const bool now = act && port != 0xffffffffu;
   const bool deferred = act && !now;
   if (valid) {
-    if (deferred) {
-      a.rec_h[i] = u32x4{H[0], H[1], H[2], H[3]};
-      a.rec_b[i] = make_uint2(H[4], v.k);
-    }
-    a.out_len[i] = now ? (uint16_t)nl : 0;
+    a.out_len[i] = act ? (uint16_t)nl : 0;
     a.pkt_slot[i] = now ? kNoSlot : slot;
     a.disposition[i] = (uint8_t)v.disp;
     a.status[i] = (uint8_t)v.st;
   }
   defer_append(a, lane, deferred, i);
-  // A5: output bytes 0..63 and their share of the TCP sum; the record
-  const uint32_t k = v.k, port_be = swap16(port & 0xffffu);
+  // A5: output bytes 0..63 and their share of the TCP sum; the record.  A
+  // deferred frame is written with source port 0 (the tail patches the port
+  // and the checksum once the batch order has assigned it).
+  const uint32_t k = v.k, port_be = now ? swap16(port & 0xffffu) : 0u;
   uint32_t O[16], accA;
-  if (!__ballot(now && k != 0u)) rows_build<true>(D, H, k, port_be, nl, O, accA);
+  if (!__ballot(act && k != 0u)) rows_build<true>(D, H, k, port_be, nl, O, accA);
   else rows_build<false>(D, H, k, port_be, nl, O, accA);
   const uint32_t span = (nl - (34u + 4u * k)) & 0xffffu;
   const uint32_t dst = be32(H[4]);
@@ -1130,7 +1127,7 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
       *reinterpret_cast<u32x4 *>(rec + 4 * m) = u32x4{O[4 * m], O[4 * m + 1], O[4 * m + 2], O[4 * m + 3]};
     const uint32_t payload = rec[17];
     *reinterpret_cast<u32x4 *>(rec + 16) =
-        u32x4{now ? nl : 0u, payload + accA, ph | (k << 16), o_off};
+        u32x4{act ? nl : 0u, payload + accA, ph | (k << 16), o_off};
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #ifndef CGPU_NAT64_ABL_NOREWRITE
@@ -1158,7 +1155,7 @@ __device__ __forceinline__ bool is_first_new(const Nat64Args &a, uint32_t i) {
   return a.pm.slots[ps & kSlotMask].w[7] == i;
 }
 
-// ---- the tail kernel: order the new keys, rewrite the deferred frames ------
+// ---- the tail kernel: order the new keys, patch the deferred frames --------
 // One small persistent grid whose workgroups take 256-packet chunk tickets.
 // For chunk b a workgroup
 //   1. counts the chunk's first packets of new keys, finds their ordinal
@@ -1166,9 +1163,11 @@ __device__ __forceinline__ bool is_first_new(const Nat64Args &a, uint32_t i) {
 //      counts (each chunk publishes its count, then looks back until it meets
 //      an inclusive prefix), and assigns port = NEXT_PORT + ordinal: the
 //      slot's port word (released), ADDR_MAP, the commit of the key;
-//   2. rewrites the chunk's deferred frames (a quad per frame), taking each
-//      frame's port from its key's slot -- assigned by this chunk or an
-//      earlier one, so a frame may wait for an earlier chunk's step 1.
+//   2. patches the chunk's deferred frames (the fused kernel rewrote them
+//      with source port 0): the port and the TCP checksum, one thread per
+//      frame, taking each frame's port from its key's slot -- assigned by
+//      this chunk or an earlier one, so a frame may wait for an earlier
+//      chunk's step 1.
 // Every wait is for a lower-numbered chunk, which a running workgroup took
 // (tickets are taken in order by running workgroups), so every wait ends.
 // The workgroup that completes the last chunk advances NEXT_PORT (after
@@ -1186,15 +1185,11 @@ __device__ __forceinline__ void reset_next_call(const Nat64Args &a) {
 __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_tail(Nat64Args a, uint32_t nb) {
   __shared__ uint32_t s_chunk, s_prefix;
   __shared__ uint32_t wcount[kBlock / 64];
-  __shared__ uint32_t s_def[kBlock];
   if (a.pm.state[4u + a.par] == 0u) {  // nothing deferred: no new key
     if (blockIdx.x == 0 && threadIdx.x == 0) reset_next_call(a);
     return;
   }
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  const uint32_t g = threadIdx.x % kFG;
-  const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
-  const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
   bool more = true;
   while (more) {
     if (threadIdx.x == 0) s_chunk = atomicAdd(&a.pm.state[6u + a.par], 1u);
@@ -1260,37 +1255,30 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_tail(Nat64Args a, uint
         __hip_atomic_store(&a.pm.slots[slot].w[6], port, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         hot_insert(a.pm, key, port);
       }
-      // 2. the chunk's deferred frames: compact them, a quad per frame
-      const bool d = ps != kNoSlot;
-      const uint64_t dm = __ballot(d);
-      const uint32_t dbelow = (uint32_t)__popcll(dm & ((1ull << lane) - 1ull));
-      __syncthreads();  // wcount reused
-      if (lane == 0) wcount[wave] = (uint32_t)__popcll(dm);
-      const uint32_t nd = (uint32_t)__syncthreads_count(d);
-      uint32_t dpre = 0;
-      for (uint32_t w = 0; w < wave; ++w) dpre += wcount[w];
-      if (d) s_def[dpre + dbelow] = i;
-      __syncthreads();
-      for (uint32_t e = threadIdx.x / kFG; e < nd; e += kBlock / kFG) {
-        const uint32_t p = s_def[e];
-        const uint32_t slot = a.pkt_slot[p] & kSlotMask;
+      // 2. the chunk's deferred frames: the fused kernel wrote them with
+      // source port 0 and the checksum c0 of that frame; set the port and
+      // patch the checksum, ~fold(~c0 + port) -- exact: the sum behind c0
+      // includes the pseudo-header's protocol 6, so it is never 0 and ~c0
+      // recovers its fold.  The port comes from the key's
+      // slot, assigned by this chunk or an earlier one (so a frame may wait
+      // for an earlier chunk's step 1).
+      if (ps != kNoSlot) {
+        const uint32_t slot = ps & kSlotMask;
         uint32_t port;
         while ((port = __hip_atomic_load(&a.pm.slots[slot].w[6], __ATOMIC_ACQUIRE,
                                          __HIP_MEMORY_SCOPE_AGENT)) == kNoPort)
           __builtin_amdgcn_s_sleep(1);
-        const u32x4 hv = a.rec_h[p];
-        const uint2 bv = a.rec_b[p];
-        FrameRec fr;
-        fr.in_off = a.off[p];
-        fr.o_off = a.out_off[p];
-        fr.new_len = (uint32_t)a.len[p] - 20u;
-        fr.info = (bv.y & 3u) | (port << 16);
-        fr.V[0] = hv[0]; fr.V[1] = hv[1]; fr.V[2] = hv[2]; fr.V[3] = hv[3]; fr.V[4] = bv.x;
-#pragma unroll
-        for (int j = 5; j < 10; ++j) fr.V[j] = 0u;
-        fr.ph = 0u;
-        rewrite_dispatch<true>(a, rs, ors, g, fr, true);
-        if (g == 0u) a.out_len[p] = (uint16_t)fr.new_len;
+        uint8_t *o = a.out_arena + a.out_off[i];
+        // the VLAN depth from the output's Ethernet header (the input's own)
+        const uint32_t marker = ((uint32_t)o[12] << 8) | o[13];
+        const uint32_t k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
+        uint8_t *t = o + 34u + 4u * k;  // the TCP header
+        const uint32_t c0 = ((uint32_t)t[16] << 8) | t[17];
+        const uint32_t c = (~fold32(((~c0) & 0xffffu) + port)) & 0xffffu;
+        t[0] = (uint8_t)(port >> 8);
+        t[1] = (uint8_t)port;
+        t[16] = (uint8_t)(c >> 8);
+        t[17] = (uint8_t)c;
       }
       // 3. done with chunk b: the last one advances NEXT_PORT
       __syncthreads();
@@ -1460,7 +1448,7 @@ uint32_t nat64_num_blocks(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 #ifndef CGPU_NAT64_TAIL_GRID
 #define CGPU_NAT64_TAIL_GRID 256
 #endif
-constexpr uint32_t kTailGrid = CGPU_NAT64_TAIL_GRID;  // workgroups of K2 / K5
+constexpr uint32_t kTailGrid = CGPU_NAT64_TAIL_GRID;  // workgroups of the tail kernel
 
 hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStream_t s) {
   // one thread per slot, ADDR_MAP entry and hot-index bucket

@@ -226,6 +226,100 @@ __device__ __forceinline__ void rows_prologue(rsrc_t rs, uint32_t off, uint32_t 
   }
 }
 
+// ---- the stream path (L4 checksum configs, waves of consecutive frames) ----
+// A wave whose 64 frames are 16-B aligned and lie in ascending,
+// non-overlapping order within kStreamMax bytes (a burst gathered into an
+// arena: IMIX in 64-B slots, 256-B frames) reads that span as one stream,
+// 1 KiB per load instruction (16 B per lane, whole lines, each line once),
+// and attributes every 16-B chunk to the frame it belongs to: a bitmap of
+// frame starts (one bit per chunk) with per-word prefix counts in LDS gives
+// a chunk's owner in two LDS reads.  A chunk is loaded only if it lies
+// before its owner's end (slot padding is skipped) and masked at that end.
+// The chunk sums are added into per-frame accumulators by a segmented scan:
+// one inclusive wave scan (DPP), then the last lane of each owner's run of
+// lanes adds its prefix and the first one subtracts the prefix before it.
+// The result is each frame's exact word sum, as the rows path produces
+// (the checksum span is that minus the words before it).  Unlike the
+// window + tail path, no line is read twice: a long frame's last line is
+// often the next frame's first, which the tail pass fetched again after
+// the window pass had let it go.
+#ifndef CGPU_PARSE_STREAM
+#define CGPU_PARSE_STREAM 1
+#endif
+constexpr uint32_t kStreamMax = 32768;  // span bytes per wave: 2048 chunks, one bitmap word per lane
+
+
+__device__ __forceinline__ uint32_t dpp_wave_shr1(uint32_t v) {  // lane l <- lane l - 1 (lane 0: 0)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_wave_shl1(uint32_t v) {  // lane l <- lane l + 1 (lane 63: 0)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
+
+// Inclusive prefix sum over the 64 lanes (row shifts, then the row
+// broadcasts of lanes 15 and 31).
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+
+// Whether the wave takes the stream path (wave-uniform); base = the first
+// frame's offset, span = bytes to the last frame's end.
+__device__ __forceinline__ bool stream_wave(uint32_t off, uint32_t len, bool valid, uint32_t lane,
+                                            uint32_t arena_len, uint32_t &base, uint32_t &span) {
+  const uint32_t noff = __shfl_down(off, 1);
+  const bool ok = valid && (off & 15u) == 0u && (lane == 63u || (noff > off && noff - off >= len));
+  if (__ballot(ok) != ~0ull || !__ballot(len > 96u)) return false;
+  base = __builtin_amdgcn_readfirstlane(off);
+  const uint32_t end = __builtin_amdgcn_readlane(off + len, 63);
+  span = end - base;
+  return span <= kStreamMax && (uint64_t)end + 16u <= (uint64_t)arena_len;
+}
+
+// Every frame's exact u16-word sum (bytes [0, len)) into s_all.  L: the
+// wave's LDS (4 x 64 dwords).
+__device__ __forceinline__ uint32_t stream_sums(rsrc_t rs, uint32_t base, uint32_t span, uint32_t off,
+                                                uint32_t len, uint32_t lane, uint32_t *L) {
+  uint32_t *bm = L, *pre = L + 64, *fend = L + 128, *acc = L + 192;
+  bm[lane] = 0u;
+  acc[lane] = 0u;
+  fend[lane] = off - base + len;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint32_t cs = (off - base) >> 4;  // the frame's first chunk
+  atomicOr(&bm[cs >> 5], 1u << (cs & 31u));
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint32_t pc = (uint32_t)__builtin_popcount(bm[lane]);
+  pre[lane] = wave_scan_incl(pc) - pc;  // frames starting before word `lane`
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint32_t nch = (span + 15u) >> 4;
+  for (uint32_t c0 = 0; c0 < nch; c0 += 64u) {
+    const uint32_t c = c0 + lane, w = c >> 5;
+    const uint32_t own = pre[w] + (uint32_t)__builtin_popcount(bm[w] & ((2u << (c & 31u)) - 1u)) - 1u;
+    const uint32_t fe = fend[own], rel = 16u * c;
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(rel < fe ? base + rel : kNoRead), 0, 0);
+    const uint32_t rem = rel < fe ? fe - rel : 16u;
+    if (__ballot(rem < 16u)) {
+#pragma unroll
+      for (uint32_t t = 0; t < 4u; ++t) {
+        const uint32_t lo = 4u * t;
+        v[t] &= rem >= lo + 4u ? 0xffffffffu : (rem <= lo ? 0u : 0xffffffffu >> (8u * (lo + 4u - rem)));
+      }
+    }
+    const uint32_t p = wave_scan_incl(sum4(v, 0u));
+    const uint32_t own_prev = dpp_wave_shr1(own), own_next = dpp_wave_shl1(own);
+    const uint32_t p_prev = dpp_wave_shr1(p);
+    if (lane == 63u || own_next != own) atomicAdd(&acc[own], p);
+    if (lane != 0u && own_prev != own) atomicSub(&acc[own], p_prev);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  return acc[lane];
+}
+
 // V4U: the accept set has no IPv6, TCP, ICMP or extension bit (the typed
 // parse::<Ipv4>() -> parse::<Udp<Ipv4>>() chain of the reference bench,
 // bench/packets.rs:65-69): every IPv6 / TCP / ICMP branch is compiled out,
@@ -249,12 +343,16 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   uint32_t wlim = 96u;  // packet bytes the window holds
   uint32_t l0_sum = 0, l0_adv = 0;  // the window line's rest, summed early (below)
   bool rows = false;     // the rows path (above): window and frame sum from rows
-  uint32_t s_all = 0;
+  bool stream = false;   // the stream path (above): frame sums from the wave's span
+  uint32_t s_all = 0, st_base = 0, st_span = 0;
 #if CGPU_PARSE_ROWS
   if (ROWS) {
+#if CGPU_PARSE_STREAM
+    stream = stream_wave(off, len, valid, threadIdx.x & 63u, a.arena_len, st_base, st_span);
+#endif
     const bool bad = valid && ((off & 15u) != 0u || (uint64_t)off + len + 16u > (uint64_t)a.arena_len);
     const uint64_t vm = __ballot(valid);
-    rows = vm && !__ballot(bad) &&
+    rows = !stream && vm && !__ballot(bad) &&
            2u * (uint32_t)__popcll(__ballot(valid && len >= 128u)) >= (uint32_t)__popcll(vm);
   }
 #endif
@@ -309,7 +407,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       // flight (at most 4, all inside the frame), and the tail starts on the
       // next line.  Frames of CGPU_PARSE_LINE0_MIN bytes and more only, where
       // the kernel is bound by HBM bytes rather than by strided requests.
-      if (L4C) {
+      if (L4C && !stream) {
         const uint32_t tb = (off + 64u) & ~15u, lb = (tb + 127u) & ~127u;
         const uint32_t nc = wlim == 64u && len >= CGPU_PARSE_LINE0_MIN && lb < off + len ? (lb - tb) >> 4 : 0u;
         if (__ballot(nc != 0u)) {
@@ -333,6 +431,13 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       for (int j = 16; j < kWin; ++j) P[j] = 0u;
     }
   }
+
+#if CGPU_PARSE_ROWS && CGPU_PARSE_STREAM
+  if (ROWS && L4C && stream) {
+    __shared__ uint32_t slds[kBlock / 64][4 * 64];
+    s_all = stream_sums(rs, st_base, st_span, off, len, threadIdx.x & 63u, slds[threadIdx.x >> 6]);
+  }
+#endif
 
   // --- Ethernet: VLAN marker at bytes 12-13 (ethernet.rs:164-181) ---------
   const uint32_t marker = be16_lo(P[3]);
@@ -475,9 +580,9 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   }
   uint32_t s = 0, stored_le = 0, t_b = 0;
   bool has_tail = false;
-  if (ROWS && L4C && l4_ok && rows) {
-    // the rows path: the same byte range's sum is the frame's word sum
-    // minus the words before it (start = 22 or 26, + 4 per VLAN tag; even)
+  if (ROWS && L4C && l4_ok && (rows || stream)) {
+    // the rows / stream paths: the same byte range's sum is the frame's word
+    // sum minus the words before it (start = 22 or 26, + 4 per VLAN tag; even)
     const uint32_t start = (v6 ? 22u : 26u) + 4u * k;
     uint32_t pre = 0;
 #pragma unroll
@@ -491,10 +596,10 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
                        : (v6 ? (Q[17] >> 16) : (Q[12] >> 16));
     s -= stored_le;
     if (icmp && !v6) s -= (Q[6] >> 16) + (Q[7] & 0xffffu) + (Q[7] >> 16) + (Q[8] & 0xffffu);
-    has_tail = len > kRowMaxLen;  // the rows summed bytes [0, kRowMaxLen)
-    t_b = off + kRowMaxLen;       // 16-B aligned: rows frames are
+    has_tail = rows && len > kRowMaxLen;  // the rows summed bytes [0, kRowMaxLen)
+    t_b = off + kRowMaxLen;               // 16-B aligned: rows frames are
   }
-  if (L4C && l4_ok && (!(ROWS && rows) || xok)) {
+  if (L4C && l4_ok && (!(ROWS && (rows || stream)) || xok)) {
     // pseudo-header addresses + span [l4, len) (udp.rs:204-219, tcp.rs:
     // 462-477, checksum.rs:56-128) are one contiguous byte range: [26, len)
     // for v4, [22, len) for v6; the stored checksum field is subtracted.

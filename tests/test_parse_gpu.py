@@ -362,3 +362,69 @@ def test_rows_path_with_checksum_tail(ctx, seed):
         assert (om & N.META_L4_CSUM_OK).sum() > 3000
         assert_parity(ctx, arena, off, ln, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP |
                       N.F_CSUM_L4 | N.F_FLOW_HASH, fields=False)
+
+
+def _stream_frames(rng, m, long_frac=0.4, max_len=1500):
+    kinds = [synth.V4_UDP, synth.V4_TCP, synth.V6_UDP, synth.V6_TCP, synth.V4_ICMP, synth.V6_ICMP]
+    frames = []
+    for _ in range(m):
+        kind = kinds[int(rng.integers(0, len(kinds)))]
+        vlan = int(rng.integers(0, 3)) if rng.random() < 0.2 else 0
+        need = 14 + 4 * vlan + (20 if kind[0] == 4 else 40) + synth.l4_header_len(kind[1])
+        L = int(rng.integers(97, max_len + 1)) if rng.random() < long_frac else int(rng.integers(need, 97))
+        fr = synth.build_frames(rng, 1, kind, max(L, need), vlan)[0]
+        r = rng.random()
+        if r < 0.04:
+            fr[int(rng.integers(0, len(fr)))] ^= 0x41
+        elif r < 0.08:
+            fr = fr[: int(rng.integers(0, len(fr) + 1))]  # truncated, down to 0 bytes
+        frames.append(bytes(fr))
+    return frames
+
+
+def _pack16(frames, gaps, tail):
+    """Frames back to back at 16-B granularity with `gaps[i]` extra 16-B
+    chunks after frame i; `tail` bytes of arena past the last frame."""
+    ln = np.array([len(f) for f in frames], np.int64)
+    step = (ln + 15) // 16 * 16 + 16 * np.asarray(gaps, np.int64)
+    step = np.maximum(step, 16)  # a 0-byte frame still takes a chunk (offsets strictly ascend)
+    off = np.concatenate([[0], np.cumsum(step)[:-1]])
+    arena = np.zeros(int(off[-1] + ln[-1] + tail), np.uint8)
+    for o, f in zip(off, frames):
+        arena[o:o + len(f)] = np.frombuffer(f, np.uint8)
+    return arena, off.astype(np.uint32), ln.astype(np.uint16)
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_stream_path_consecutive_frames(ctx, seed):
+    """The stream path (parse.hip: waves of ascending 16-B aligned frames
+    within 32 KiB, read as one span and summed per frame by a segmented
+    scan): frames of 0..1500 B back to back at 16-B granularity, with and
+    without padding chunks between them, every kind, VLAN, ICMP, truncated
+    and corrupted frames, spans right at the 32 KiB limit, an arena ending
+    16 B and 0 B past the last frame (the second falls back), and a batch
+    whose waves are not in ascending order (they fall back): bit-exact."""
+    rng = np.random.default_rng(seed)
+    frames = _stream_frames(rng, 6400)
+    n = len(frames)
+    cases = [np.zeros(n, np.int64), rng.integers(0, 3, n)]
+    for gaps in cases:
+        for tail in (16, 0):
+            arena, off, ln = _pack16(frames, gaps, tail)
+            assert 128 <= len(arena) // n <= 2200  # the variant with the stream path
+            for flags in (ALL | N.F_ACCEPT_ICMP, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP |
+                          N.F_CSUM_L4 | N.F_FLOW_HASH):
+                om = assert_parity(ctx, arena, off, ln, flags, fields=bool(flags & N.F_ACCEPT_V6))
+            assert (om & N.META_L4_CSUM_OK).sum() > 1000
+    # 64 frames of 512 B (32 KiB, the limit) per wave, then 513 B (over it: rows)
+    for L in (512 - 16, 512, 513):
+        fr = [bytes(x) for x in synth.build_frames(rng, 1024, synth.V6_TCP, L, 0)]
+        arena, off, ln = _pack16(fr, np.zeros(1024, np.int64), 16)
+        om = assert_parity(ctx, arena, off, ln, ALL)
+        assert (om & N.META_L4_CSUM_OK).all()
+    # waves whose offsets are not ascending: the window + tail path
+    arena, off, ln = _pack16(frames, cases[1], 16)
+    perm = np.arange(n)
+    for w in range(0, n - 64, 64):
+        perm[w + 3], perm[w + 40] = perm[w + 40], perm[w + 3]
+    assert_parity(ctx, arena, off[perm], ln[perm], ALL)
