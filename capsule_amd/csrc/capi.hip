@@ -621,13 +621,6 @@ int cgpu_parse_mbufs(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32_t fla
   return parse_staged(ctx, n, get, flags, meta, csum, flow_hash, fields);
 }
 
-// The hot index (kernels.hpp HotBucket): 2^hot_log2 buckets of three
-// entries, a quarter of the slots up to 2^15 buckets (2 MiB, room for the
-// 65536 gateway ports' worth of keys at half load).
-#ifndef CGPU_HOT_LOG2_MAX
-#define CGPU_HOT_LOG2_MAX 15
-#endif
-
 int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_port,
                         cgpu_portmap **out) {
   if (!ctx || !out || capacity_log2 < 4 || capacity_log2 > 29) return fail(CGPU_EINVAL);
@@ -635,10 +628,7 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
   DeviceGuard dg(ctx->device);
   if (!dg.ok()) return fail(CGPU_ENODEV);
   const size_t cap = (size_t)1 << capacity_log2;
-  const uint32_t hot_log2 = capacity_log2 - 2 < CGPU_HOT_LOG2_MAX ? capacity_log2 - 2 : CGPU_HOT_LOG2_MAX;
-  const size_t hot = (size_t)1 << hot_log2;
-  const size_t o_rev = 256, o_hot = o_rev + 65536 * sizeof(cgpu::RevEntry);
-  const size_t o_slots = o_hot + hot * sizeof(cgpu::HotBucket);
+  const size_t o_rev = 256, o_slots = o_rev + 65536 * sizeof(cgpu::RevEntry);
   const size_t bytes = o_slots + cap * sizeof(cgpu::PortSlot);
   void *mem = nullptr;
   if (hipMalloc(&mem, bytes) != hipSuccess) return fail(CGPU_ENOMEM);
@@ -652,11 +642,8 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
   uint8_t *p = (uint8_t *)mem;
   pm->dev.state = (uint32_t *)p;
   pm->dev.rev = (cgpu::RevEntry *)(p + o_rev);
-  pm->dev.hot = (cgpu::HotBucket *)(p + o_hot);
   pm->dev.slots = (cgpu::PortSlot *)(p + o_slots);
   pm->dev.cap_mask = (uint32_t)(cap - 1);
-  pm->dev.hot_mask = (uint32_t)(hot - 1);
-  pm->dev.hot_shift = 32u - hot_log2;
   if (hipEventCreateWithFlags(&pm->done, hipEventDisableTiming) != hipSuccess) {
     (void)hipFree(mem);
     delete pm;

@@ -55,33 +55,12 @@ struct RevEntry {
   uint32_t w[8];
 };
 
-// The hot index: a dense, bucketed copy of the committed PORT_MAP entries
-// (key -> assigned port; a committed key's port never changes), 64-B
-// buckets of three entries.  It exists because the authoritative table is
-// sized for its capacity, so its committed keys are spread one per line
-// over a table much larger than the L2; here they sit three to a bucket.
-//   w[0]                 bits 0-7: entries in this bucket (0..3; 4 = full
-//                        and overflowed into the next bucket); bits 8 + 8j:
-//                        an 8-bit fingerprint of entry j's key
-//   w[1 + 5j .. 4 + 5j]  entry j < 3: v6 source address
-//   w[5 + 5j]            v6-side TCP source port | assigned port << 16
-// A lookup reads w[0] first (one dword, issued early), then only the entry
-// whose fingerprint matches (a second read of a line just fetched).
-struct HotBucket {
-  uint32_t w[16];
-};
-constexpr uint32_t kHotWays = 3u;
-constexpr uint32_t kHotProbes = 4u;  // buckets an insert / a lookup visits at most
-
 struct PortMapDev {
   PortSlot *slots;  // [cap]
   RevEntry *rev;    // [65536] (ADDR_MAP)
-  HotBucket *hot;   // [hot_mask + 1]
   uint32_t *state;  // [11]: next_port, entries, -, -, deferred[2], chunk tickets[2],
                     // batch new keys, chunks ordered[2]
   uint32_t cap_mask;
-  uint32_t hot_mask;
-  uint32_t hot_shift;  // bucket = (key hash * golden) >> hot_shift
 };
 
 struct Nat64Args {

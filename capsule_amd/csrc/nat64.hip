@@ -22,9 +22,9 @@
 //     at the shifted position;
 //   - DPP quad broadcasts give every lane the header dwords; each lane
 //     classifies by the reference control flow (Act / Drop / Abort);
-//   - lane 0 looks the key up in the device port map (6to4: the hot index,
-//     then the open-addressing PORT_MAP; 4to6: the ADDR_MAP array, one 32-B
-//     value per gateway port, read by the whole quad);
+//   - lane 0 looks the key up in the device port map (6to4: the
+//     open-addressing PORT_MAP; 4to6: the ADDR_MAP array, one 32-B value per
+//     gateway port, read by the whole quad);
 //   - each lane patches its chunks in registers and sums its part of the TCP
 //     span with v_sad_u16; the quad reduces; the lane holding the TCP
 //     checksum field stores it last.
@@ -157,6 +157,17 @@ __device__ __forceinline__ void classify(rsrc_t rs, uint32_t arena_len, uint32_t
                                          uint32_t len, uint32_t room, V6 &v) {
   constexpr int NW = 20;
   uint32_t P[NW];
+  if ((off & 3u) == 0u && (uint64_t)off + 80u <= (uint64_t)arena_len) {
+    // a dword-aligned frame well inside the arena: five 16-B loads (bytes
+    // past the frame's end are never used: classify checks len first)
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u * c), 0, 0);
+      P[4 * c] = t[0]; P[4 * c + 1] = t[1]; P[4 * c + 2] = t[2]; P[4 * c + 3] = t[3];
+    }
+    classify_dwords(P, len, room, v);
+    return;
+  }
   const uint32_t sh = off & 3u, base = off - sh;
   const uint32_t need = sh + (len < 80u ? len : 80u);
   uint32_t D[NW + 1];
@@ -281,117 +292,14 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, rsrc_t rs,
     }
     if (match) {
       if (ref & kPersist) return h;
-      atomicMin(&a.pm.slots[h].w[7], i);
+      // the key's first packet index (w[7] only decreases, so a value loaded
+      // with the slot that is already below i makes the atomic moot)
+      if (claimed || s1[3] > i) atomicMin(&a.pm.slots[h].w[7], i);
       return h | kLocalBit;
     }
     h = (h + 1u) & a.pm.cap_mask;
   }
   return kNoSlot;
-}
-
-// ---- the hot index (kernels.hpp HotBucket) ------------------------------------
-// A committed key is found in one 64-B bucket (rarely the next ones, when an
-// insert found its bucket full): its header dword, then the one entry whose
-// fingerprint matches.  A miss is final once a bucket has not overflowed:
-// the key was never inserted past it.  Every miss falls back to the
-// authoritative table, so the index only ever short-cuts a lookup whose
-// answer is fixed (a committed key's port never changes).
-constexpr uint32_t kHotFull = 4u;  // bucket count value: full, overflowed
-
-__device__ __forceinline__ uint32_t hot_bucket(const PortMapDev &pm, uint32_t hraw) {
-  return (hraw * 0x9e3779b1u) >> pm.hot_shift;
-}
-
-__device__ __forceinline__ uint32_t hot_fp(uint32_t hraw) {
-  return ((hraw * 0x85ebca6bu) >> 11) & 0xffu;
-}
-
-// Bucket b with header dword w0: true and the port if the key is there;
-// `more` when the bucket overflowed (look in the next one).  Only entries
-// whose fingerprint matches are read: one read for almost every lookup (a
-// false match costs a second), so a wave waits for one round trip.
-__device__ __forceinline__ bool hot_in_bucket(const PortMapDev &pm, uint32_t b, uint32_t w0,
-                                              const uint32_t (&key)[5], uint32_t fp,
-                                              uint32_t &port, bool &more) {
-  const uint32_t cnt = w0 & 0xffu;
-  more = cnt > kHotWays;
-  uint32_t cand = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < kHotWays; ++j)
-    if (j < cnt && ((w0 >> (8u + 8u * j)) & 0xffu) == fp) cand |= 1u << j;
-  while (cand) {
-    const uint32_t j = __builtin_ctz(cand);
-    cand &= cand - 1u;
-    const uint32_t *e = pm.hot[b].w + 1u + 5u * j;
-    const u32x4 k4 = *reinterpret_cast<const u32x4 *>(e);  // dword-aligned
-    const uint32_t k5 = e[4];
-    if (k4[0] == key[0] && k4[1] == key[1] && k4[2] == key[2] && k4[3] == key[3] &&
-        (k5 & 0xffffu) == key[4]) {
-      port = k5 >> 16;
-      return true;
-    }
-  }
-  return false;
-}
-
-// The whole lookup, given the first bucket's header dword.
-__device__ __forceinline__ bool hot_find(const PortMapDev &pm, const uint32_t (&key)[5], uint32_t hraw,
-                                         uint32_t w0, uint32_t &port) {
-  const uint32_t fp = hot_fp(hraw);
-  uint32_t b = hot_bucket(pm, hraw);
-  for (uint32_t t = 0;;) {
-    bool more;
-    if (hot_in_bucket(pm, b, w0, key, fp, port, more)) return true;
-    if (!more || ++t == kHotProbes) return false;
-    b = (b + 1u) & pm.hot_mask;
-    w0 = pm.hot[b].w[0];
-  }
-}
-
-// Insert a key just committed with its port (the tail kernel; lookups of it
-// start with the next call).  An entry is claimed by a CAS on the bucket's
-// header (count + 1, the key's fingerprint); a full bucket is marked
-// overflowed and the key tries the next; after kHotProbes buckets the key
-// stays in the authoritative table only.
-__device__ __forceinline__ void hot_insert(const PortMapDev &pm, const uint32_t (&key)[5],
-                                           uint32_t port) {
-  const uint32_t hraw = key_hash(key), fp = hot_fp(hraw);
-  uint32_t b = hot_bucket(pm, hraw);
-  for (uint32_t t = 0; t < kHotProbes; ++t) {
-    uint32_t *hw = &pm.hot[b].w[0];
-    uint32_t old = __hip_atomic_load(hw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), c;
-    for (;;) {
-      c = old & 0xffu;
-      if (c >= kHotFull) break;
-      const uint32_t nw = c < kHotWays ? old + 1u + (fp << (8u + 8u * c)) : old + 1u;
-      const uint32_t prev = atomicCAS(hw, old, nw);
-      if (prev == old) break;
-      old = prev;
-    }
-    if (c < kHotWays) {
-      uint32_t *e = pm.hot[b].w + 1u + 5u * c;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) e[j] = key[j];
-      e[4] = key[4] | (port << 16);
-      return;
-    }
-    b = (b + 1u) & pm.hot_mask;
-  }
-}
-
-// assigned_port (main.rs:41-53) lookup for frame i with the key's hash: the
-// hot index first, then the authoritative table (probe_port_at).
-// (CGPU_NAT64_NO_HOT: A/B build without the hot-index lookups; the tail
-// still fills the index.)
-__device__ __forceinline__ uint32_t probe_port_key(const Nat64Args &a, rsrc_t rs, uint32_t i,
-                                                   const uint32_t (&key)[5], uint32_t hraw,
-                                                   uint32_t &port) {
-#ifndef CGPU_NAT64_NO_HOT
-  if (hot_find(a.pm, key, hraw, a.pm.hot[hot_bucket(a.pm, hraw)].w[0], port)) return 0u;
-#endif
-  const uint32_t h = hraw & a.pm.cap_mask;
-  const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
-  return probe_port_at(a, rs, i, key, h, sp[0], sp[1], port);
 }
 
 // assigned_port (main.rs:41-53) lookup for frame i: returns the table slot
@@ -402,7 +310,9 @@ __device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, rsrc_t rs, ui
                                                uint32_t &port) {
   uint32_t key[5];
   make_key(v, key);
-  return probe_port_key(a, rs, i, key, key_hash(key), port);
+  const uint32_t h = key_hash(key) & a.pm.cap_mask;
+  const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
+  return probe_port_at(a, rs, i, key, h, sp[0], sp[1], port);
 }
 
 // ---- the rewrite of one frame by its quad (the fused kernel's quad path) -----
@@ -1047,17 +957,14 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   const bool act0 = valid && v.disp == CGPU_ACT;
   uint32_t key[5];
   make_key(v, key);
-  const uint32_t hraw = key_hash(key);
-  uint32_t hw0 = 0u;
-#if defined(CGPU_NAT64_NO_HOT)
+  const uint32_t h = key_hash(key) & a.pm.cap_mask;
   u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
+#ifndef CGPU_NAT64_ABL_NOPROBE
   if (act0) {
-    const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[hraw & a.pm.cap_mask]);
+    const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
     s0 = sp[0];
     s1 = sp[1];
   }
-#elif !defined(CGPU_NAT64_ABL_NOPROBE)
-  if (act0) hw0 = a.pm.hot[hot_bucket(a.pm, hraw)].w[0];  // the key's hot bucket header, examined after B1
 #endif
   const uint32_t nl = len - 20u;  // meaningful for ACT frames
   if (mine) {
@@ -1077,20 +984,7 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     slot = 0u;
     port = 1025u;
 #else
-    // the hot index; on a miss (a key new in this batch, or one the index
-    // has no room for) the authoritative table
-#ifdef CGPU_NAT64_NO_HOT
-    (void)hw0;
-    slot = probe_port_at(a, rs, i, key, hraw & a.pm.cap_mask, s0, s1, port);
-#else
-    if (hot_find(a.pm, key, hraw, hw0, port)) {
-      slot = 0u;
-    } else {
-      const uint32_t h = hraw & a.pm.cap_mask;
-      const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
-      slot = probe_port_at(a, rs, i, key, h, sp[0], sp[1], port);
-    }
-#endif
+    slot = probe_port_at(a, rs, i, key, h, s0, s1, port);
 #endif
   }
   if (v.disp == CGPU_ACT && slot == kNoSlot) {
@@ -1204,26 +1098,41 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_tail(Nat64Args a, uint
       const uint32_t below = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
       if (lane == 0) wcount[wave] = (uint32_t)__popcll(mask);
       const uint32_t c = (uint32_t)__syncthreads_count(f);
-      if (threadIdx.x == 0) {
+      if (wave == 0) {
+        // decoupled look-back by the whole wave: lane l reads chunk
+        // j0 - l's word (64 predecessors per round trip), the nearest
+        // inclusive prefix ends the walk
         const uint64_t ep = (uint64_t)(a.epoch & 0x3fffffffu) << 34;
+        if (lane == 0)
+          __hip_atomic_store(&a.lookback[b], ep | (b == 0 ? kLbIncl : kLbAgg) | c, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
         uint32_t prefix = 0;
-        if (b == 0) {
-          __hip_atomic_store(&a.lookback[0], ep | kLbIncl | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          __hip_atomic_store(&a.lookback[b], ep | kLbAgg | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          for (uint32_t j = b - 1;; --j) {
-            uint64_t v;
+        for (uint32_t j0 = b; j0 > 0; j0 = j0 > 64u ? j0 - 64u : 0u) {
+          const bool has = lane < j0;
+          const uint32_t j = j0 - 1u - (has ? lane : 0u);
+          uint64_t v = kLbIncl;  // lanes past chunk 0: an empty inclusive prefix
+          if (has) {
             do {
               v = __hip_atomic_load(&a.lookback[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } while ((v & ~0x3ffffffffull) != ep || (v & (3ull << 32)) == 0ull);
-            prefix += (uint32_t)v;
-            if (v & kLbIncl) break;
           }
-          __hip_atomic_store(&a.lookback[b], ep | kLbIncl | (prefix + c), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t incl = __ballot(has && (v & kLbIncl));
+          // the nearest inclusive prefix (lowest lane) and the aggregates before it
+          const uint32_t stop = incl ? (uint32_t)__builtin_ctzll(incl) : 63u;
+          uint32_t x = has && lane <= stop ? (uint32_t)v : 0u;
+#pragma unroll
+          for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d);
+          prefix += x;
+          if (incl) break;
         }
-        s_prefix = prefix;
-        if (b == nb - 1u) a.pm.state[8] = prefix + c;  // the batch's new keys
+        if (lane == 0) {
+          if (b != 0)
+            __hip_atomic_store(&a.lookback[b], ep | kLbIncl | (prefix + c), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          s_prefix = prefix;
+          if (b == nb - 1u)  // the batch's new keys, for the workgroup that finishes last
+            __hip_atomic_store(&a.pm.state[8], prefix + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
       __syncthreads();
       uint32_t pre = s_prefix;
@@ -1248,12 +1157,12 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_tail(Nat64Args a, uint
             e.w[4] = key[4] | kRevValid;
           }
         }
-        // PORT_MAP.insert_new (main.rs:49): commit the key for later batches,
-        // and copy it into the hot index
+        // PORT_MAP.insert_new (main.rs:49): commit the key for later batches
         a.pm.slots[slot].w[7] = 0xffffffffu;
         a.pm.slots[slot].w[0] = kPersist;
-        __hip_atomic_store(&a.pm.slots[slot].w[6], port, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        hot_insert(a.pm, key, port);
+        // the port itself is all its readers (step 2, any workgroup) use:
+        // a write-through store, no release fence
+        __hip_atomic_store(&a.pm.slots[slot].w[6], port, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       // 2. the chunk's deferred frames: the fused kernel wrote them with
       // source port 0 and the checksum c0 of that frame; set the port and
@@ -1265,7 +1174,7 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_tail(Nat64Args a, uint
       if (ps != kNoSlot) {
         const uint32_t slot = ps & kSlotMask;
         uint32_t port;
-        while ((port = __hip_atomic_load(&a.pm.slots[slot].w[6], __ATOMIC_ACQUIRE,
+        while ((port = __hip_atomic_load(&a.pm.slots[slot].w[6], __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT)) == kNoPort)
           __builtin_amdgcn_s_sleep(1);
         uint8_t *o = a.out_arena + a.out_off[i];
@@ -1283,10 +1192,15 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_tail(Nat64Args a, uint
       // 3. done with chunk b: the last one advances NEXT_PORT
       __syncthreads();
       if (threadIdx.x == 0) {
-        const uint32_t old = __hip_atomic_fetch_add(&a.pm.state[9u + a.par], 1u, __ATOMIC_ACQ_REL,
+        // Every read of NEXT_PORT in this chunk is done (the barrier above
+        // waited for them); the write-through store of state[8] is drained
+        // before the count that makes another workgroup read it (no
+        // release / acquire fences: they write back / invalidate the L2).
+        __builtin_amdgcn_s_waitcnt(0);
+        const uint32_t old = __hip_atomic_fetch_add(&a.pm.state[9u + a.par], 1u, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
         if (old == nb - 1u) {  // every chunk has read NEXT_PORT: advance it (AtomicU16 wrap)
-          const uint32_t total = a.pm.state[8];
+          const uint32_t total = __hip_atomic_load(&a.pm.state[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           a.pm.state[0] = (a.pm.state[0] + total) & 0xffffu;
           a.pm.state[1] += total;
           reset_next_call(a);
@@ -1344,11 +1258,231 @@ __device__ __forceinline__ void classify4(const uint32_t (&P)[20], uint32_t len,
   }
 }
 
-__global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_4to6_fused(Nat64Args a) {
-  const uint32_t g = threadIdx.x & (kFG - 1u);
-  const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
-  const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
-  QuadDesc d = quad_desc<false>(a, blockIdx.x * (kBlock / kFG) + threadIdx.x / kFG);
+// The IPv6 header of a 4to6 frame (Ipv6Header::default + set_dscp / ecn /
+// next_header / hop_limit / src / dst, main.rs:92-105; payload_length by
+// Ipv6::reconcile, v6/mod.rs:331-334) as 10 LE dwords, from its IPv4
+// classification and its ADDR_MAP value (the original v6 source address
+// s0); ph = the LE residue of the pseudo-header's address words.
+__device__ __forceinline__ void ipv6_header(const V4 &v, uint32_t nl, u32x4 s0, uint32_t (&V)[10],
+                                            uint32_t &ph) {
+  const uint32_t de = (v.L[0] >> 8) & 0xffu;            // dscp_ecn (v4.rs:186-203)
+  const uint32_t dscp = de >> 2, ecn = de & 3u;
+  const uint32_t hop = ((v.L[2] & 0xffu) - 1u) & 0xffu;  // ttl - 1 (u8, wrapping)
+  const uint32_t w = (6u << 28) | ((dscp << 22) & 0x0fc00000u) | ((ecn << 20) & 0x00300000u);
+  V[0] = be32(w);
+  V[1] = swap16((nl - v.eth_len - 40u) & 0xffffu) | (6u << 16) | (hop << 24);
+  V[2] = 0x9bff6400u;  // 64:ff9b::/96 (map4to6, main.rs:62-74)
+  V[3] = 0u;
+  V[4] = 0u;
+  V[5] = v.L[3];       // v4 source address
+  V[6] = s0[0];        // the ADDR_MAP value: the original v6 source
+  V[7] = s0[1];
+  V[8] = s0[2];
+  V[9] = s0[3];
+  uint32_t x = sad16(V[2], 0u);
+  x = sad16(V[5], x);
+  x = sad16(s0[0], sad16(s0[1], sad16(s0[2], sad16(s0[3], x))));
+  ph = fold32(x);
+}
+
+// assigned_addr(port) (main.rs:56-58) and the push's tailroom check for a
+// frame the classification left ACT: ADDR_MAP holds the value, one 32-B
+// entry per gateway port.
+__device__ __forceinline__ void addr_map_check(const Nat64Args &a, uint32_t len, u32x4 s1, V4 &v) {
+  if (!(s1[0] & kRevValid)) {
+    v.disp = CGPU_DROP;  // no mapping: Either::Drop
+  } else if (len >= a.room - 20u) {  // push::<Ipv6>(): extend 40 needs 40 < tailroom
+    v.st = CGPU_PKT_NOT_RESIZED;
+    v.disp = CGPU_ABORT;
+  }
+}
+
+// ---- 4to6 rows path -----------------------------------------------------------
+// The 6to4 rows design mirrored: every frame of the wave 16-B aligned in the
+// input, dword-aligned in the output and at most 236 B long (output at most
+// 256 B, one row pass).  Row j loads frame 4r + j in round r, four whole
+// frames per load instruction; bytes 0..95 reach the frame's own lane through
+// LDS, which classifies it by nat_4to6's control flow, reads its ADDR_MAP
+// entry (issued here, examined after B1) and builds output bytes 0..79
+// (Ethernet, the IPv6 header, the TCP header with the original port, the
+// checksum field zero) into an LDS record.  B1: output chunk l >= 5 is
+// in(l-2).w, in(l-1).xyz (DPP row shifts right: the frame grows by 20 B
+// behind the new header) and its TCP sum a DPP row reduction.  B2: row j
+// stores frame 4r + j in one instruction; lanes 0-4 take the record, lane 4
+// with the TCP checksum patched in (output bytes 70 + 4k).
+constexpr uint32_t kRowW6 = 24;  // LDS dwords per 4to6 record: output bytes 0..79 + 4 meta
+
+// Output dwords 0..19 of the rewritten frame (header-relative r = w - k)
+// and the TCP sum (LE words) of the span bytes among them.
+template <bool K0>
+__device__ __forceinline__ void rows_build6(const uint32_t (&D)[24], const uint32_t (&V)[10],
+                                            uint32_t k, uint32_t port_be, uint32_t nl,
+                                            uint32_t (&O)[20], uint32_t &acc) {
+  acc = 0;
+#pragma unroll
+  for (int w = 0; w < 20; ++w) {
+    const int r = w - (K0 ? 0 : (int)k);
+    const uint32_t x = w < 8 ? D[w] : D[w - 5];  // output bytes >= 32: input - 20
+    const uint32_t d = out_dword<false>(r, x, V, port_be);
+    uint32_t m = r < 13 ? 0u : (r == 13 ? 0xffff0000u : 0xffffffffu);
+    m &= range_mask(4u * (uint32_t)w, 0u, nl);
+    acc = sad16(d & m, acc);
+    O[w] = d;
+  }
+}
+
+// B1 (4to6): output chunks 5.. from the row's input chunks, and their sum.
+template <bool UNI>
+__device__ __forceinline__ void rows_payload6(u32x4 (&X)[kRowFrames / 4], uint32_t *lds, uint32_t row,
+                                              uint32_t l, uint32_t nl0) {
+  u32x4 M0;
+#pragma unroll
+  for (uint32_t t = 0; t < 4u; ++t) M0[t] = range_mask(16u * l + 4u * t, 0u, nl0);
+#pragma unroll
+  for (uint32_t r = 0; r < kRowFrames / 4u; ++r) {
+    uint32_t *fr = lds + (4u * r + row) * kRowW6;
+    const uint32_t fnl = fr[20];
+    if (!__ballot(fnl != 0u)) continue;  // no ACT frame in this round
+    const u32x4 A = X[r];
+    u32x4 o;
+    o[0] = dppz<kRowShr2>(A[3]);
+    o[1] = dppz<kRowShr1>(A[0]);
+    o[2] = dppz<kRowShr1>(A[1]);
+    o[3] = dppz<kRowShr1>(A[2]);
+    uint32_t acc = 0;
+    if (l >= 5u) {
+#pragma unroll
+      for (uint32_t t = 0; t < 4u; ++t)
+        acc = sad16(o[t] & (UNI ? M0[t] : range_mask(16u * l + 4u * t, 0u, fnl)), acc);
+    }
+    acc += dppz<kRowShr1>(acc);
+    acc += dppz<kRowShr2>(acc);
+    acc += dppz<kRowShr4>(acc);
+    acc += dppz<kRowShr8>(acc);
+    if (l == 15u) fr[21] = acc;
+    X[r] = o;
+  }
+}
+
+// B2 (4to6): lanes 0-4 the record's chunks, lanes 5.. the payload; lane 4
+// patches the checksum (record meta: fnl, TCP sum, fph_be | k << 16, o_off).
+__device__ __forceinline__ void rows_store6(const Nat64Args &a, rsrc_t ors, const u32x4 (&X)[kRowFrames / 4],
+                                            const uint32_t *lds, uint32_t row, uint32_t l) {
+#pragma unroll
+  for (uint32_t r = 0; r < kRowFrames / 4u; ++r) {
+    const uint32_t *fr = lds + (4u * r + row) * kRowW6;
+    const u32x4 meta = *reinterpret_cast<const u32x4 *>(fr + 20);
+    const uint32_t fnl = meta[0];
+    if (!__ballot(fnl != 0u)) continue;
+    const u32x4 hc = *reinterpret_cast<const u32x4 *>(fr + 4u * (l < 5u ? l : 0u));
+    u32x4 o = l < 5u ? hc : X[r];
+    if (l == 4u) {
+      const uint32_t fk = meta[2] >> 16, fph = meta[2] & 0xffffu;
+      const uint32_t tcp_c = (~fold32(fph + swap16(fold32(meta[1])))) & 0xffffu;
+#pragma unroll
+      for (uint32_t t = 0; t < 4u; ++t)
+        if (t == fk + 1u) o[t] |= swap16(tcp_c) << 16;
+    }
+    if (fnl != 0u) {
+      const uint32_t b0 = 16u * l;
+      if (b0 + 16u <= fnl) __builtin_amdgcn_raw_buffer_store_b128(o, ors, (int)(meta[3] + b0), 0, kRowAux);
+      else if (b0 < fnl) store_chunk<true>(ors, a.out_arena, meta[3], l, o, fnl);
+    }
+  }
+}
+
+__device__ __forceinline__ bool rows_4to6(const Nat64Args &a, rsrc_t rs, rsrc_t ors, uint32_t base,
+                                          uint32_t lane, uint32_t *lds) {
+  constexpr uint32_t R = kRowFrames / 4u;  // rounds
+  const uint32_t i = base + lane;
+  const bool mine = lane < kRowFrames;
+  const bool valid = mine && i < a.n;
+  const uint32_t off = valid ? a.off[i] : 0u;
+  const uint32_t len = valid ? (uint32_t)a.len[i] : 0u;
+  const uint32_t o_off = valid ? a.out_off[i] : 0u;
+  if (__ballot(valid && ((off & 15u) != 0u || (o_off & 3u) != 0u || len > 236u))) return false;
+  const uint32_t row = lane >> 4, l = lane & 15u;
+  // A2: the frames in rows, four whole frames per load instruction
+  u32x4 X[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t f = 4u * r + row;
+    const uint32_t fo = __shfl(off, (int)f), fl = __shfl(len, (int)f);
+    X[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * l < fl ? fo + 16u * l : kNoRead), 0, kRowLdAux);
+  }
+  // A1: bytes 0..95 of every frame, through LDS to the frame's own lane
+  uint32_t D[24];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r)
+    if (l < 6u) *reinterpret_cast<u32x4 *>(lds + (4u * r + row) * 24u + 4u * l) = X[r];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+  for (uint32_t m = 0; m < 6u; ++m) {
+    const u32x4 t = *reinterpret_cast<const u32x4 *>(lds + (mine ? lane : 0u) * 24u + 4u * m);
+    D[4 * m] = t[0]; D[4 * m + 1] = t[1]; D[4 * m + 2] = t[2]; D[4 * m + 3] = t[3];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  uint32_t *rec = lds + (mine ? lane : 0u) * kRowW6;
+  // A3: nat_4to6's control flow; the ADDR_MAP entry is read now and examined
+  // after B1
+  uint32_t P[20];
+#pragma unroll
+  for (int j = 0; j < 20; ++j) P[j] = D[j];
+  V4 v;
+  classify4(P, len, v);
+  const bool act0 = valid && v.disp == CGPU_ACT;
+  u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
+  if (act0) {
+    const u32x4 *rp = reinterpret_cast<const u32x4 *>(&a.pm.rev[v.gw_port]);
+    s0 = rp[0];
+    s1 = rp[1];
+  }
+  const uint32_t nl = len + 20u;  // meaningful for ACT frames
+  if (mine) {
+    rec[20] = act0 ? nl : 0u;
+    rec[23] = o_off;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // B1: realign and sum the payload of every round (lookup-independent)
+  const uint32_t nl0 = __shfl(nl, (int)(__builtin_ctzll(__ballot(act0) | (1ull << 63))));
+  if (!__ballot(act0 && nl != nl0)) rows_payload6<true>(X, lds, row, l, nl0);
+  else rows_payload6<false>(X, lds, row, l, nl0);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // A4: the ADDR_MAP value, the IPv6 header
+  if (act0) addr_map_check(a, len, s1, v);
+  const bool act = valid && v.disp == CGPU_ACT;
+  if (valid) {
+    a.out_len[i] = act ? (uint16_t)nl : 0;
+    a.disposition[i] = (uint8_t)v.disp;
+    a.status[i] = (uint8_t)v.st;
+  }
+  uint32_t V[10], ph;
+  ipv6_header(v, nl, s0, V, ph);
+  // A5: output bytes 0..79 and their share of the TCP sum; the record
+  const uint32_t k = v.k, port_be = swap16(s1[0] & 0xffffu);  // the original v6-side port
+  uint32_t O[20], accA;
+  if (!__ballot(act && k != 0u)) rows_build6<true>(D, V, k, port_be, nl, O, accA);
+  else rows_build6<false>(D, V, k, port_be, nl, O, accA);
+  const uint32_t span = (nl - (54u + 4u * k)) & 0xffffu;
+  // the pseudo-header in the big-endian domain of the final fold
+  const uint32_t fph = fold32(swap16(ph) + span + 6u);
+  if (mine) {
+#pragma unroll
+    for (int m = 0; m < 5; ++m)
+      *reinterpret_cast<u32x4 *>(rec + 4 * m) = u32x4{O[4 * m], O[4 * m + 1], O[4 * m + 2], O[4 * m + 3]};
+    const uint32_t payload = rec[21];
+    *reinterpret_cast<u32x4 *>(rec + 20) = u32x4{act ? nl : 0u, payload + accA, fph | (k << 16), o_off};
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  rows_store6(a, ors, X, lds, row, l);
+  return true;
+}
+
+// The general 4to6 path: one quad per frame (any alignment, any length).
+__device__ __forceinline__ void quad_4to6(const Nat64Args &a, rsrc_t rs, rsrc_t ors, uint32_t i,
+                                          uint32_t lane) {
+  const uint32_t g = lane & (kFG - 1u);
+  QuadDesc d = quad_desc<false>(a, i);
   quad_modes<false>(a, d);
   const bool al16 = d.fast && !__ballot(d.nl != 0u && (d.off & 15u) != 0u);
   u32x4 X[kFJ], Y, Y4;
@@ -1359,20 +1493,13 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_4to6_fused(Nat64Args a
   gather_header(Y, Y4, P);
   V4 v;
   classify4(P, d.len, v);
-  // assigned_addr(port) (main.rs:56-58): ADDR_MAP holds the value, one 32-B
-  // entry per gateway port; the quad's lanes read the same words (one
-  // request per quad)
+  // assigned_addr(port): the quad's lanes read the same words (one request)
   u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
   if (d.valid && v.disp == CGPU_ACT) {
     const u32x4 *rp = reinterpret_cast<const u32x4 *>(&a.pm.rev[v.gw_port]);
     s0 = rp[0];
     s1 = rp[1];
-    if (!(s1[0] & kRevValid)) {
-      v.disp = CGPU_DROP;  // no mapping: Either::Drop
-    } else if (d.len >= a.room - 20u) {  // push::<Ipv6>(): extend 40 needs 40 < tailroom
-      v.st = CGPU_PKT_NOT_RESIZED;
-      v.disp = CGPU_ABORT;
-    }
+    addr_map_check(a, d.len, s1, v);
   }
   const bool act = d.valid && v.disp == CGPU_ACT;
   if (d.valid && g == 0u) {
@@ -1385,29 +1512,27 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_4to6_fused(Nat64Args a
   f.in_off = d.off;
   f.o_off = d.o_off;
   f.new_len = d.nl;
-  const uint32_t de = (v.L[0] >> 8) & 0xffu;            // dscp_ecn (v4.rs:186-203)
-  const uint32_t dscp = de >> 2, ecn = de & 3u;
-  const uint32_t hop = ((v.L[2] & 0xffu) - 1u) & 0xffu;  // ttl - 1 (u8, wrapping)
-  // Ipv6Header::default + set_dscp/ecn/next_header/hop_limit/src/dst
-  const uint32_t w = (6u << 28) | ((dscp << 22) & 0x0fc00000u) | ((ecn << 20) & 0x00300000u);
-  f.V[0] = be32(w);
-  f.V[1] = swap16((d.nl - v.eth_len - 40u) & 0xffffu) | (6u << 16) | (hop << 24);
-  f.V[2] = 0x9bff6400u;  // 64:ff9b::/96 (map4to6, main.rs:62-74)
-  f.V[3] = 0u;
-  f.V[4] = 0u;
-  f.V[5] = v.L[3];       // v4 source address
-  // V6..V9: the ADDR_MAP key, the original v6 source
-  f.V[6] = s0[0];
-  f.V[7] = s0[1];
-  f.V[8] = s0[2];
-  f.V[9] = s0[3];
-  uint32_t ph = 0;       // v6 pseudo-header addresses, LE residue
-  ph = sad16(f.V[2], ph);
-  ph = sad16(f.V[5], ph);
-  ph = sad16(s0[0], sad16(s0[1], sad16(s0[2], sad16(s0[3], ph))));
-  f.ph = fold32(ph);
+  ipv6_header(v, d.nl, s0, f.V, f.ph);
   f.info = v.k | kNow | ((s1[0] & 0xffffu) << 16);  // the original v6-side port
   rewrite_quad<false>(a, rs, ors, g, d, al16, f, X, E);
+}
+
+#ifndef CGPU_NAT64_4TO6_WPE
+#define CGPU_NAT64_4TO6_WPE 4
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CGPU_NAT64_4TO6_WPE)))
+void nat64_4to6_fused(Nat64Args a) {
+  __shared__ uint32_t lds[kBlock / 64][kRowFrames * kRowW6];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t base = (blockIdx.x * (kBlock / 64u) + wave) * kRowFrames;
+  if (base >= a.n) return;  // wave-uniform
+  const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
+  const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
+#ifndef CGPU_NAT64_4TO6_ROWS  // A/B knob: 0 = every wave takes the quad path
+#define CGPU_NAT64_4TO6_ROWS 1
+#endif
+  if (CGPU_NAT64_4TO6_ROWS && rows_4to6(a, rs, ors, base, lane, lds[wave])) return;
+  for (uint32_t q = 0; q < kRowFrames / 16u; ++q) quad_4to6(a, rs, ors, base + 16u * q + lane / 4u, lane);
 }
 
 __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
@@ -1420,11 +1545,6 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
   if (i < 65536u) {
     u32x4 *r = reinterpret_cast<u32x4 *>(&pm.rev[i]);
     r[0] = r[1] = u32x4{0u, 0u, 0u, 0u};
-  }
-  if (i <= pm.hot_mask) {
-    u32x4 *h = reinterpret_cast<u32x4 *>(&pm.hot[i]);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) h[c] = u32x4{0u, 0u, 0u, 0u};
   }
   if (i == 0) {
     pm.state[0] = first_port;
@@ -1451,7 +1571,7 @@ uint32_t nat64_num_blocks(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 constexpr uint32_t kTailGrid = CGPU_NAT64_TAIL_GRID;  // workgroups of the tail kernel
 
 hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStream_t s) {
-  // one thread per slot, ADDR_MAP entry and hot-index bucket
+  // one thread per slot and ADDR_MAP entry
   const uint32_t cap = pm.cap_mask + 1u > 65536u ? pm.cap_mask + 1u : 65536u;
   hipLaunchKernelGGL(portmap_init, dim3((cap + 255) / 256), dim3(256), 0, s, pm, first_port);
   return hipGetLastError();
@@ -1471,8 +1591,8 @@ hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s) {
 
 hipError_t launch_nat64_4to6(const Nat64Args &a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  const uint32_t nbf = (a.n + kBlock / kFG - 1) / (kBlock / kFG);
-  hipLaunchKernelGGL(nat64_4to6_fused, dim3(nbf), dim3(kBlock), 0, s, a);  // one quad per frame
+  const uint32_t fpb = (kBlock / 64u) * kRowFrames;  // kRowFrames frames per wave
+  hipLaunchKernelGGL(nat64_4to6_fused, dim3((a.n + fpb - 1) / fpb), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 

@@ -281,13 +281,39 @@ __device__ __forceinline__ bool stream_wave(uint32_t off, uint32_t len, bool val
   return span <= kStreamMax && (uint64_t)end + 16u <= (uint64_t)arena_len;
 }
 
-// Every frame's exact u16-word sum (bytes [0, len)) into s_all.  L: the
-// wave's LDS (4 x 64 dwords).
-__device__ __forceinline__ uint32_t stream_sums(rsrc_t rs, uint32_t base, uint32_t span, uint32_t off,
-                                                uint32_t len, uint32_t lane, uint32_t *L) {
-  uint32_t *bm = L, *pre = L + 64, *fend = L + 128, *acc = L + 192;
+// One 64-chunk step of the stream: chunk c of the span (relative to base)
+// for this lane, its owner frame and that frame's end.
+struct StreamChunk {
+  uint32_t c, own, fe;
+};
+
+// Chunks at or past `hi` (the end of the half's range) take the owner of
+// chunk hi - 1: a valid frame of the half, whose sum they add 0 to (they are
+// not loaded).  Their own bitmap word may lie past the bitmap.
+__device__ __forceinline__ StreamChunk stream_chunk(const uint32_t *bm, const uint32_t *pre,
+                                                    const uint32_t *fend, uint32_t c, uint32_t hi) {
+  const uint32_t q = c < hi ? c : hi - 1u, w = q >> 5;
+  StreamChunk k;
+  k.c = c;
+  k.own = pre[w] + (uint32_t)__builtin_popcount(bm[w] & ((2u << (q & 31u)) - 1u)) - 1u;
+  k.fe = fend[k.own];
+  return k;
+}
+
+// Every frame's window P (bytes 0..95) and exact u16-word sum s_all (bytes
+// [0, len)) from the wave's span.  The frames are taken in two halves of 32
+// (the windows of one half in LDS at a time); within a half the span is read
+// 2 KiB per step (two loads in flight per lane).  L: the wave's LDS,
+// kStreamLds dwords.
+constexpr uint32_t kStreamLds = 5u * 64u + kRowHalf * kWin;
+
+__device__ __forceinline__ void stream_prologue(rsrc_t rs, uint32_t base, uint32_t span, uint32_t off,
+                                                uint32_t len, uint32_t lane, uint32_t *L,
+                                                uint32_t (&P)[kWin], uint32_t &s_all) {
+  uint32_t *bm = L, *pre = L + 64, *fst = L + 128, *fend = L + 192, *acc = L + 256, *win = L + 320;
   bm[lane] = 0u;
   acc[lane] = 0u;
+  fst[lane] = off - base;
   fend[lane] = off - base + len;
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint32_t cs = (off - base) >> 4;  // the frame's first chunk
@@ -295,29 +321,63 @@ __device__ __forceinline__ uint32_t stream_sums(rsrc_t rs, uint32_t base, uint32
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint32_t pc = (uint32_t)__builtin_popcount(bm[lane]);
   pre[lane] = wave_scan_incl(pc) - pc;  // frames starting before word `lane`
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint32_t nch = (span + 15u) >> 4;
-  for (uint32_t c0 = 0; c0 < nch; c0 += 64u) {
-    const uint32_t c = c0 + lane, w = c >> 5;
-    const uint32_t own = pre[w] + (uint32_t)__builtin_popcount(bm[w] & ((2u << (c & 31u)) - 1u)) - 1u;
-    const uint32_t fe = fend[own], rel = 16u * c;
-    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(rel < fe ? base + rel : kNoRead), 0, 0);
-    const uint32_t rem = rel < fe ? fe - rel : 16u;
-    if (__ballot(rem < 16u)) {
+  const uint32_t mid = __builtin_amdgcn_readlane(cs, (int)kRowHalf);  // half 1's first chunk
 #pragma unroll
-      for (uint32_t t = 0; t < 4u; ++t) {
-        const uint32_t lo = 4u * t;
-        v[t] &= rem >= lo + 4u ? 0xffffffffu : (rem <= lo ? 0u : 0xffffffffu >> (8u * (lo + 4u - rem)));
+  for (uint32_t half = 0; half < 2u; ++half) {
+    const uint32_t lo = half ? mid : 0u, hi = half ? nch : mid;
+#pragma unroll
+    for (uint32_t m = 0; m < kRowHalf * kWin / 256u; ++m)
+      *reinterpret_cast<u32x4 *>(win + 4u * (64u * m + lane)) = u32x4{0u, 0u, 0u, 0u};
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (uint32_t c0 = lo; c0 < hi; c0 += 128u) {
+      StreamChunk k[2];
+      u32x4 v[2];
+#pragma unroll
+      for (uint32_t u = 0; u < 2u; ++u) {
+        k[u] = stream_chunk(bm, pre, fend, c0 + 64u * u + lane, hi);
+        const uint32_t rel = 16u * k[u].c;
+        const bool in = k[u].c < hi && rel < k[u].fe;
+        v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(in ? base + rel : kNoRead), 0, 0);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 2u; ++u) {
+        const uint32_t rel = 16u * k[u].c;
+        const uint32_t rem = k[u].c < hi && rel < k[u].fe ? k[u].fe - rel : 16u;
+        if (__ballot(rem < 16u)) {
+#pragma unroll
+          for (uint32_t t = 0; t < 4u; ++t) {
+            const uint32_t b = 4u * t;
+            v[u][t] &= rem >= b + 4u ? 0xffffffffu : (rem <= b ? 0u : 0xffffffffu >> (8u * (b + 4u - rem)));
+          }
+        }
+        // bytes 0..95 of a frame of this half: its window
+        const uint32_t pos = rel - fst[k[u].own], fh = k[u].own - kRowHalf * half;
+        if (k[u].c < hi && pos < 96u && fh < kRowHalf)
+          *reinterpret_cast<u32x4 *>(win + fh * kWin + (pos >> 2)) = v[u];
+        const uint32_t p = wave_scan_incl(sum4(v[u], 0u));
+        const uint32_t own = k[u].own;
+        const uint32_t own_prev = dpp_wave_shr1(own), own_next = dpp_wave_shl1(own);
+        const uint32_t p_prev = dpp_wave_shr1(p);
+        if (lane == 63u || own_next != own) atomicAdd(&acc[own], p);
+        if (lane != 0u && own_prev != own) atomicSub(&acc[own], p_prev);
       }
     }
-    const uint32_t p = wave_scan_incl(sum4(v, 0u));
-    const uint32_t own_prev = dpp_wave_shr1(own), own_next = dpp_wave_shl1(own);
-    const uint32_t p_prev = dpp_wave_shr1(p);
-    if (lane == 63u || own_next != own) atomicAdd(&acc[own], p);
-    if (lane != 0u && own_prev != own) atomicSub(&acc[own], p_prev);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if ((lane >> 5) == half) {
+      const uint32_t fh = lane & (kRowHalf - 1u);
+#pragma unroll
+      for (int m = 0; m < kWin / 4; ++m) {
+        const u32x4 t = *reinterpret_cast<const u32x4 *>(win + fh * kWin + 4u * m);
+        P[4 * m] = t[0];
+        P[4 * m + 1] = t[1];
+        P[4 * m + 2] = t[2];
+        P[4 * m + 3] = t[3];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  return acc[lane];
+  s_all = acc[lane];
 }
 
 // V4U: the accept set has no IPv6, TCP, ICMP or extension bit (the typed
@@ -347,20 +407,30 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   uint32_t s_all = 0, st_base = 0, st_span = 0;
 #if CGPU_PARSE_ROWS
   if (ROWS) {
-#if CGPU_PARSE_STREAM
-    stream = stream_wave(off, len, valid, threadIdx.x & 63u, a.arena_len, st_base, st_span);
-#endif
     const bool bad = valid && ((off & 15u) != 0u || (uint64_t)off + len + 16u > (uint64_t)a.arena_len);
     const uint64_t vm = __ballot(valid);
-    rows = !stream && vm && !__ballot(bad) &&
+    rows = vm && !__ballot(bad) &&
            2u * (uint32_t)__popcll(__ballot(valid && len >= 128u)) >= (uint32_t)__popcll(vm);
+#if CGPU_PARSE_STREAM
+    // waves of mostly long frames keep the rows (as fast, fewer VALU per
+    // byte); the stream takes mixed waves (IMIX), whose short frames would
+    // leave 12 of a row's 16 lanes idle
+    stream = !rows && stream_wave(off, len, valid, threadIdx.x & 63u, a.arena_len, st_base, st_span);
+#endif
   }
 #endif
   const bool slow = (off & 3u) != 0u || (uint64_t)off + 96u > (uint64_t)a.arena_len;
+#if CGPU_PARSE_ROWS
+  constexpr uint32_t kPathLds = kRowLds > kStreamLds ? kRowLds : kStreamLds;
+  __shared__ uint32_t rlds[ROWS ? kBlock / 64 : 1][ROWS ? kPathLds : 1];
+#endif
   if (ROWS && rows) {
 #if CGPU_PARSE_ROWS
-    __shared__ uint32_t rlds[kBlock / 64][kRowLds];
     rows_prologue(rs, valid ? off : 0u, valid ? len : 0u, threadIdx.x & 63u, rlds[threadIdx.x >> 6], P, s_all);
+#endif
+  } else if (ROWS && stream) {
+#if CGPU_PARSE_ROWS && CGPU_PARSE_STREAM
+    stream_prologue(rs, st_base, st_span, off, len, threadIdx.x & 63u, rlds[threadIdx.x >> 6], P, s_all);
 #endif
   } else if (__ballot(slow)) {
     load_window_general(rs, a.arena_len, off, len, P);
@@ -407,7 +477,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       // flight (at most 4, all inside the frame), and the tail starts on the
       // next line.  Frames of CGPU_PARSE_LINE0_MIN bytes and more only, where
       // the kernel is bound by HBM bytes rather than by strided requests.
-      if (L4C && !stream) {
+      if (L4C) {
         const uint32_t tb = (off + 64u) & ~15u, lb = (tb + 127u) & ~127u;
         const uint32_t nc = wlim == 64u && len >= CGPU_PARSE_LINE0_MIN && lb < off + len ? (lb - tb) >> 4 : 0u;
         if (__ballot(nc != 0u)) {
@@ -431,13 +501,6 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       for (int j = 16; j < kWin; ++j) P[j] = 0u;
     }
   }
-
-#if CGPU_PARSE_ROWS && CGPU_PARSE_STREAM
-  if (ROWS && L4C && stream) {
-    __shared__ uint32_t slds[kBlock / 64][4 * 64];
-    s_all = stream_sums(rs, st_base, st_span, off, len, threadIdx.x & 63u, slds[threadIdx.x >> 6]);
-  }
-#endif
 
   // --- Ethernet: VLAN marker at bytes 12-13 (ethernet.rs:164-181) ---------
   const uint32_t marker = be16_lo(P[3]);

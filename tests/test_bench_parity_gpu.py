@@ -88,7 +88,7 @@ def test_bench_nat64_config_every_byte(ctx):
     """BASELINE config 4 exactly as benched: the 1 M x 256-B stream through
     a map of the bench's capacity (bench.PORTMAP_LOG2), first pass (every
     key new: the nat64_cold config) and the steady-state pass the timed loop
-    repeats (every key known, looked up through the hot index); all output
+    repeats (every key known); all output
     bytes, lengths, dispositions and the port map state equal the oracle's.
     Then a cold pass again after cgpu_portmap_reset (how nat64_cold times
     it), and the replies through 4to6 (the nat64_4to6 bench config)."""

@@ -262,15 +262,14 @@ def _nat_both(ctx, gw, pm, direction, arena, off, ln, out_off, size):
     return ref
 
 
-def test_hot_index_overflow_falls_back(ctx):
-    """A map whose hot index (kernels.hpp HotBucket) is far too small for its
-    keys (16 buckets of three entries for 30 keys), so buckets overflow,
-    lookups walk overflow chains and some keys are found only in the
-    authoritative table; then 200 keys in a 128-bucket index.  Ports, frames and the replies through 4to6 still
-    equal the oracle's over several batches."""
+def test_small_maps_near_their_load_limit(ctx):
+    """Port maps close to their capacity (30 keys in 64 slots, 200 in 512):
+    long linear-probe chains, claims racing for neighbouring slots.  Ports,
+    frames and the replies through 4to6 equal the oracle's over several
+    batches (first pass: every key new; then every lookup a committed key)."""
     from capsule_amd import packets
 
-    gw = packets.Nat64Gateway(ctx, capacity_log2=6)  # 64 slots, 2^(6-2) = 16 hot buckets
+    gw = packets.Nat64Gateway(ctx, capacity_log2=6)  # 64 slots
     pm = oracle_lib.PortMap()
     a, o, l = synth.nat64_stream(3000, n_keys=30, seed=52, drop_frac=0.05)
     for _ in range(3):  # first pass: keys new; then every lookup through the index
@@ -280,8 +279,7 @@ def test_hot_index_overflow_falls_back(ctx):
     o6 = (np.arange(len(ro), dtype=np.int64) * 256).astype(np.uint32)
     _nat_both(ctx, gw, pm, "4to6", ra, ro, rl, o6, 256 * len(ro) + 64)
     gw.close()
-    # 200 keys in a 128-bucket index (384 entries, at most 4 buckets probed)
-    gw = packets.Nat64Gateway(ctx, capacity_log2=9)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=9)  # 512 slots
     pm = oracle_lib.PortMap()
     a, o, l = synth.nat64_stream(6000, n_keys=200, seed=53)
     for _ in range(3):
