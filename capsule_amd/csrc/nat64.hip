@@ -1566,7 +1566,7 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
 uint32_t nat64_num_blocks(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 
 #ifndef CGPU_NAT64_TAIL_GRID
-#define CGPU_NAT64_TAIL_GRID 256
+#define CGPU_NAT64_TAIL_GRID 1024
 #endif
 constexpr uint32_t kTailGrid = CGPU_NAT64_TAIL_GRID;  // workgroups of the tail kernel
 

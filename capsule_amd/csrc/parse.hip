@@ -246,6 +246,10 @@ __device__ __forceinline__ void rows_prologue(rsrc_t rs, uint32_t off, uint32_t 
 #ifndef CGPU_PARSE_STREAM
 #define CGPU_PARSE_STREAM 1
 #endif
+#ifndef CGPU_STREAM_U
+#define CGPU_STREAM_U 3
+#endif
+constexpr uint32_t kStreamU = CGPU_STREAM_U;  // 1 KiB loads in flight per lane and step
 constexpr uint32_t kStreamMax = 32768;  // span bytes per wave: 2048 chunks, one bitmap word per lane
 
 
@@ -303,7 +307,7 @@ __device__ __forceinline__ StreamChunk stream_chunk(const uint32_t *bm, const ui
 // Every frame's window P (bytes 0..95) and exact u16-word sum s_all (bytes
 // [0, len)) from the wave's span.  The frames are taken in two halves of 32
 // (the windows of one half in LDS at a time); within a half the span is read
-// 2 KiB per step (two loads in flight per lane).  L: the wave's LDS,
+// kStreamU KiB per step (kStreamU loads in flight per lane).  L: the wave's LDS,
 // kStreamLds dwords.
 constexpr uint32_t kStreamLds = 5u * 64u + kRowHalf * kWin;
 
@@ -330,18 +334,18 @@ __device__ __forceinline__ void stream_prologue(rsrc_t rs, uint32_t base, uint32
     for (uint32_t m = 0; m < kRowHalf * kWin / 256u; ++m)
       *reinterpret_cast<u32x4 *>(win + 4u * (64u * m + lane)) = u32x4{0u, 0u, 0u, 0u};
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (uint32_t c0 = lo; c0 < hi; c0 += 128u) {
-      StreamChunk k[2];
-      u32x4 v[2];
+    for (uint32_t c0 = lo; c0 < hi; c0 += 64u * kStreamU) {
+      StreamChunk k[kStreamU];
+      u32x4 v[kStreamU];
 #pragma unroll
-      for (uint32_t u = 0; u < 2u; ++u) {
+      for (uint32_t u = 0; u < kStreamU; ++u) {
         k[u] = stream_chunk(bm, pre, fend, c0 + 64u * u + lane, hi);
         const uint32_t rel = 16u * k[u].c;
         const bool in = k[u].c < hi && rel < k[u].fe;
         v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(in ? base + rel : kNoRead), 0, 0);
       }
 #pragma unroll
-      for (uint32_t u = 0; u < 2u; ++u) {
+      for (uint32_t u = 0; u < kStreamU; ++u) {
         const uint32_t rel = 16u * k[u].c;
         const uint32_t rem = k[u].c < hi && rel < k[u].fe ? k[u].fe - rel : 16u;
         if (__ballot(rem < 16u)) {
