@@ -458,6 +458,12 @@ static int parse_zero_copy(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32
                        (uint32_t *)(D + lay.off), (uint16_t *)(D + lay.len), dcnt, 0, nullptr,
                        0, s) != hipSuccess)
         return fail(CGPU_EIO);
+      // The parse is queued behind the gather without waiting for its
+      // cursor: in the common case the chunk fits and one sync serves both.
+      // On an overflow (a chunk of frames larger than the arena so far, e.g.
+      // the first burst from a jumbo mempool) the frames past `cap` were not
+      // gathered, and the results this pass wrote for the chunk are
+      // overwritten by the retry below; only that rare chunk is parsed twice.
       if (int e = parse_and_return(ctx, ctx->d_zc, cap, m, lay, flags, meta, csum, flow_hash,
                                    fields, at))
         return e;
@@ -508,6 +514,7 @@ static int parse_frames_zero_copy(cgpu_ctx *ctx, const uint8_t *const *pkt, cons
                               ctx->d_zc, cap, (uint32_t *)(D + lay.off), (uint16_t *)(D + lay.len),
                               dcnt, s) != hipSuccess)
         return fail(CGPU_EIO);
+      // parsed before the cursor is read back: see parse_zero_copy
       if (int e = parse_and_return(ctx, ctx->d_zc, cap, m, lay, flags, meta, csum, flow_hash,
                                    fields, at))
         return e;
