@@ -428,3 +428,58 @@ def test_stream_path_consecutive_frames(ctx, seed):
     for w in range(0, n - 64, 64):
         perm[w + 3], perm[w + 40] = perm[w + 40], perm[w + 3]
     assert_parity(ctx, arena, off[perm], ln[perm], ALL)
+
+
+def _pack64(frames, gaps, tail, misalign=()):
+    """Frames in 64-B slots (the bench's IMIX arena, the ingress gather's
+    layout) with `gaps[i]` extra empty slots after frame i; frames whose
+    index is in `misalign` start 16 B into their slot."""
+    ln = np.array([len(f) for f in frames], np.int64)
+    step = (ln + 63) // 64 * 64 + 64 * np.asarray(gaps, np.int64)
+    step = np.maximum(step, 64) + 64  # room for a 16-B shift
+    off = np.concatenate([[0], np.cumsum(step)[:-1]])
+    off[list(misalign)] += 16
+    arena = np.full(int(off[-1] + ln[-1] + tail), 0x5a, np.uint8)  # slot padding is not zero
+    for o, f in zip(off, frames):
+        arena[o:o + len(f)] = np.frombuffer(f, np.uint8)
+    return arena, off.astype(np.uint32), ln.astype(np.uint16)
+
+
+@pytest.mark.parametrize("seed", [7, 8])
+def test_stream_path_64b_slots(ctx, seed):
+    """The stream path over frames in 64-B slots, the layout of the bench's
+    IMIX arena and of the ingress gather: frames of 0..1500 B with non-zero
+    slot padding (loaded with the frame's last chunk or skipped, never summed)
+    and 0..2 empty slots between them, every kind, VLAN, ICMP, truncated and
+    corrupted frames; waves with one frame 16 B into its slot; mixed waves
+    just under and just over the 32 KiB span limit: bit-exact."""
+    rng = np.random.default_rng(seed)
+    frames = _stream_frames(rng, 6400)
+    n = len(frames)
+    for gaps in (np.zeros(n, np.int64), rng.integers(0, 3, n)):
+        for mis in ((), tuple(range(5, n, 128))):
+            arena, off, ln = _pack64(frames, gaps, 16, mis)
+            assert 128 <= len(arena) // n <= 2200  # the variant with the stream path
+            for flags in (ALL | N.F_ACCEPT_ICMP, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP |
+                          N.F_CSUM_L4 | N.F_FLOW_HASH):
+                om = assert_parity(ctx, arena, off, ln, flags, fields=bool(flags & N.F_ACCEPT_V6))
+            assert (om & N.META_L4_CSUM_OK).sum() > 1000
+    # waves of k 1000-B frames in 1024-B slots and 64 - k 64-B frames (k < 32:
+    # not the rows path): k = 29 spans 31,936 B (streamed), k = 31 33,856 B
+    # (over the 32 KiB limit: the window + tail path)
+    for k in (29, 31):
+        fr, off, o = [], [], 0
+        for w in range(16):
+            longs = set(rng.choice(64, k, replace=False).tolist())
+            for j in range(64):
+                L = 1000 if j in longs else 64
+                kind = synth.V6_TCP if L == 1000 else synth.V4_UDP
+                fr.append(bytes(synth.build_frames(rng, 1, kind, L, 0)[0]))
+                off.append(o)
+                o += 1024 if L == 1000 else 64
+        arena = np.full(o + 16, 0x5a, np.uint8)
+        for a0, f in zip(off, fr):
+            arena[a0:a0 + len(f)] = np.frombuffer(f, np.uint8)
+        ln = np.array([len(f) for f in fr], np.uint16)
+        om = assert_parity(ctx, arena, np.array(off, np.uint32), ln, ALL)
+        assert (om & N.META_L4_CSUM_OK).all()
