@@ -45,19 +45,19 @@ struct PortSlot {
   uint32_t w[8];
 };
 
-// ADDR_MAP (main.rs:38: CHashMap<u16, (Ipv6Addr, u16)>) as a dense array
-// indexed by gateway port that holds the value itself, 32 bytes per port
-// (2 MiB): a 4to6 lookup is one 32-B read, with no dependent load.
-//   w[0..3]  v6 source address (wire bytes as LE dwords)
-//   w[4]     v6-side TCP source port | kRevValid
+// ADDR_MAP (main.rs:38: CHashMap<u16, (Ipv6Addr, u16)>) as two dense arrays
+// indexed by gateway port that hold the value itself: the v6 source address
+// (16 B, wire bytes as LE dwords) and the v6-side TCP source port with a
+// valid bit (4 B).  A 4to6 lookup is two independent reads, no dependent
+// load; split this way, 50,000 mapped ports occupy 7,800 lines (1 MiB)
+// instead of 12,500 with one 32-B entry per port, so more of them stay in
+// the XCD's L2 against the frame stream.
 constexpr uint32_t kRevValid = 0x10000u;
-struct RevEntry {
-  uint32_t w[8];
-};
 
 struct PortMapDev {
   PortSlot *slots;  // [cap]
-  RevEntry *rev;    // [65536] (ADDR_MAP)
+  u32x4 *rev_addr;     // [65536] (ADDR_MAP: address)
+  uint32_t *rev_port;  // [65536] (ADDR_MAP: port | kRevValid)
   uint32_t *state;  // [11]: next_port, entries, -, -, deferred[2], chunk tickets[2],
                     // batch new keys, chunks ordered[2]
   uint32_t cap_mask;

@@ -23,8 +23,8 @@
 //   - DPP quad broadcasts give every lane the header dwords; each lane
 //     classifies by the reference control flow (Act / Drop / Abort);
 //   - lane 0 looks the key up in the device port map (6to4: the
-//     open-addressing PORT_MAP; 4to6: the ADDR_MAP array, one 32-B value per
-//     gateway port, read by the whole quad);
+//     open-addressing PORT_MAP; 4to6: the ADDR_MAP arrays, a 16-B address
+//     and a 4-B port per gateway port, read by the whole quad);
 //   - each lane patches its chunks in registers and sums its part of the TCP
 //     span with v_sad_u16; the quad reduces; the lane holding the TCP
 //     checksum field stores it last.
@@ -1150,12 +1150,9 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_tail(Nat64Args a, uint
         // o + 65536k share a port, so only its first lap (o < 65536) can be
         // first, and only if no earlier call mapped the port: one writer per
         // entry, no race.
-        if (ordinal < 65536u) {
-          RevEntry &e = a.pm.rev[port];
-          if (!(e.w[4] & kRevValid)) {
-            *reinterpret_cast<u32x4 *>(&e.w[0]) = u32x4{key[0], key[1], key[2], key[3]};
-            e.w[4] = key[4] | kRevValid;
-          }
+        if (ordinal < 65536u && !(a.pm.rev_port[port] & kRevValid)) {
+          a.pm.rev_addr[port] = u32x4{key[0], key[1], key[2], key[3]};
+          a.pm.rev_port[port] = key[4] | kRevValid;
         }
         // PORT_MAP.insert_new (main.rs:49): commit the key for later batches
         a.pm.slots[slot].w[7] = 0xffffffffu;
@@ -1212,8 +1209,9 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_tail(Nat64Args a, uint
 }
 
 // ============================ 4to6 direction =================================
-// Classify, look the TCP destination port up in ADDR_MAP (rev[port] = the
-// v6 key itself, one 32-B read), build the IPv6 header, then the quad
+// Classify, look the TCP destination port up in ADDR_MAP (rev_addr[port],
+// rev_port[port] = the v6 key itself, two independent reads), build the
+// IPv6 header, then the quad
 // rewrite with the input shifted by -20 bytes behind the 40-byte header (the
 // TCP checksum field, output bytes 70+4k, is in chunk 4).
 // 4to6 classification of one frame (main.rs:86-118) up to the ADDR_MAP
@@ -1286,10 +1284,10 @@ __device__ __forceinline__ void ipv6_header(const V4 &v, uint32_t nl, u32x4 s0, 
 }
 
 // assigned_addr(port) (main.rs:56-58) and the push's tailroom check for a
-// frame the classification left ACT: ADDR_MAP holds the value, one 32-B
-// entry per gateway port.
-__device__ __forceinline__ void addr_map_check(const Nat64Args &a, uint32_t len, u32x4 s1, V4 &v) {
-  if (!(s1[0] & kRevValid)) {
+// frame the classification left ACT: ADDR_MAP holds the value (the port
+// word: the v6-side port and the valid bit).
+__device__ __forceinline__ void addr_map_check(const Nat64Args &a, uint32_t len, uint32_t rport, V4 &v) {
+  if (!(rport & kRevValid)) {
     v.disp = CGPU_DROP;  // no mapping: Either::Drop
   } else if (len >= a.room - 20u) {  // push::<Ipv6>(): extend 40 needs 40 < tailroom
     v.st = CGPU_PKT_NOT_RESIZED;
@@ -1431,11 +1429,11 @@ __device__ __forceinline__ bool rows_4to6(const Nat64Args &a, rsrc_t rs, rsrc_t 
   V4 v;
   classify4(P, len, v);
   const bool act0 = valid && v.disp == CGPU_ACT;
-  u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
+  u32x4 s0 = {0u, 0u, 0u, 0u};
+  uint32_t rport = 0u;
   if (act0) {
-    const u32x4 *rp = reinterpret_cast<const u32x4 *>(&a.pm.rev[v.gw_port]);
-    s0 = rp[0];
-    s1 = rp[1];
+    s0 = a.pm.rev_addr[v.gw_port];
+    rport = a.pm.rev_port[v.gw_port];
   }
   const uint32_t nl = len + 20u;  // meaningful for ACT frames
   if (mine) {
@@ -1449,7 +1447,7 @@ __device__ __forceinline__ bool rows_4to6(const Nat64Args &a, rsrc_t rs, rsrc_t 
   else rows_payload6<false>(X, lds, row, l, nl0);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   // A4: the ADDR_MAP value, the IPv6 header
-  if (act0) addr_map_check(a, len, s1, v);
+  if (act0) addr_map_check(a, len, rport, v);
   const bool act = valid && v.disp == CGPU_ACT;
   if (valid) {
     a.out_len[i] = act ? (uint16_t)nl : 0;
@@ -1459,7 +1457,7 @@ __device__ __forceinline__ bool rows_4to6(const Nat64Args &a, rsrc_t rs, rsrc_t 
   uint32_t V[10], ph;
   ipv6_header(v, nl, s0, V, ph);
   // A5: output bytes 0..79 and their share of the TCP sum; the record
-  const uint32_t k = v.k, port_be = swap16(s1[0] & 0xffffu);  // the original v6-side port
+  const uint32_t k = v.k, port_be = swap16(rport & 0xffffu);  // the original v6-side port
   uint32_t O[20], accA;
   if (!__ballot(act && k != 0u)) rows_build6<true>(D, V, k, port_be, nl, O, accA);
   else rows_build6<false>(D, V, k, port_be, nl, O, accA);
@@ -1494,12 +1492,12 @@ __device__ __forceinline__ void quad_4to6(const Nat64Args &a, rsrc_t rs, rsrc_t 
   V4 v;
   classify4(P, d.len, v);
   // assigned_addr(port): the quad's lanes read the same words (one request)
-  u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
+  u32x4 s0 = {0u, 0u, 0u, 0u};
+  uint32_t rport = 0u;
   if (d.valid && v.disp == CGPU_ACT) {
-    const u32x4 *rp = reinterpret_cast<const u32x4 *>(&a.pm.rev[v.gw_port]);
-    s0 = rp[0];
-    s1 = rp[1];
-    addr_map_check(a, d.len, s1, v);
+    s0 = a.pm.rev_addr[v.gw_port];
+    rport = a.pm.rev_port[v.gw_port];
+    addr_map_check(a, d.len, rport, v);
   }
   const bool act = d.valid && v.disp == CGPU_ACT;
   if (d.valid && g == 0u) {
@@ -1513,7 +1511,7 @@ __device__ __forceinline__ void quad_4to6(const Nat64Args &a, rsrc_t rs, rsrc_t 
   f.o_off = d.o_off;
   f.new_len = d.nl;
   ipv6_header(v, d.nl, s0, f.V, f.ph);
-  f.info = v.k | kNow | ((s1[0] & 0xffffu) << 16);  // the original v6-side port
+  f.info = v.k | kNow | ((rport & 0xffffu) << 16);  // the original v6-side port
   rewrite_quad<false>(a, rs, ors, g, d, al16, f, X, E);
 }
 
@@ -1543,8 +1541,8 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
     s[1] = u32x4{0u, 0u, 0u, 0xffffffffu};
   }
   if (i < 65536u) {
-    u32x4 *r = reinterpret_cast<u32x4 *>(&pm.rev[i]);
-    r[0] = r[1] = u32x4{0u, 0u, 0u, 0u};
+    pm.rev_addr[i] = u32x4{0u, 0u, 0u, 0u};
+    pm.rev_port[i] = 0u;
   }
   if (i == 0) {
     pm.state[0] = first_port;
