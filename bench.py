@@ -708,39 +708,50 @@ def main():
 
 
 def bench_nat64_mbufs(args, w):
-    """End-to-end nat64 6to4 over rte_mbuf bursts (cgpu_nat64_mbufs): the
-    device reads the frames from the registered mempool, rewrites them and
-    writes the ACT frames back into their mbufs, one synchronous call per
-    burst.  The call rewrites the mempool in place, so the pool is restored
-    between calls, outside the timed region (only the calls are timed).
-    Prints one JSON line."""
+    """End-to-end nat64 over rte_mbuf bursts (cgpu_nat64_mbufs, or
+    cgpu_nat64_frames over (data_address, data_len) pairs): the device reads
+    the frames from the registered mempool, rewrites them and writes the ACT
+    frames back into their mbufs, one synchronous call per burst.  6to4 for
+    --config nat64; 4to6 for --config nat64_4to6, over the replies to the
+    6to4 stream, whose pass (untimed, device-resident) populates the map.
+    The call rewrites the mempool in place, so the pool is restored between
+    calls, outside the timed region (only the calls are timed).  Prints one
+    JSON line."""
     import torch
 
     from capsule_amd import packets, synth
 
-    n = len(w["off"])
     ctx = packets.Context(0)
+    to6 = args.config == "nat64_4to6"
+    direction = "4to6" if to6 else "6to4"
+    if to6:  # the replies (host arrays), the map populated by their 6to4 pass
+        gw = nat64_4to6_setup(w, ctx, torch.device("cuda", 0))
+    n = len(w["off"])
     room = 2048  # DPDK's default data room: 4to6 needs the tailroom
     stride = (128 + 128 + room + 63) // 64 * 64
     pinned = torch.zeros(stride * n, dtype=torch.uint8, pin_memory=True)
     mem, mbufs = synth.mbuf_pool(w["arena"], w["off"], w["len"], mem=pinned.numpy(), room=room)
     orig = mem.copy()
     reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
-    gw = packets.Nat64Gateway(ctx, capacity_log2=PORTMAP_LOG2)
+    if not to6:
+        gw = packets.Nat64Gateway(ctx, capacity_log2=PORTMAP_LOG2)
     B = min(args.burst, n)
     bursts = [mbufs[s:s + B] for s in range(0, n - B + 1, B)]
     frames = args.ingress == "frames"
     if frames:  # (data_address, data_len) pairs, as the RX core hands them over
         fa, fl = synth.mbuf_frames(mem, mbufs)
-        pairs = [(fa[s:s + B].copy(), fl[s:s + B].copy()) for s in range(0, n - B + 1, B)]
+        tr = synth.mbuf_tailroom(mem, mbufs)
+        pairs = [(fa[s:s + B].copy(), fl[s:s + B].copy(), tr[s:s + B].copy())
+                 for s in range(0, n - B + 1, B)]
 
     def call(k):
         if frames:
-            _, d, _ = gw.nat_frames(*pairs[k % len(pairs)], direction="6to4")
+            a, ln, t = pairs[k % len(pairs)]
+            _, d, _ = gw.nat_frames(a, ln, t if to6 else None, direction=direction)
             return d
-        return gw.nat_mbufs(bursts[k % len(bursts)], "6to4")[0]
+        return gw.nat_mbufs(bursts[k % len(bursts)], direction)[0]
 
-    call(0)  # first sight of the keys (deferred path), untimed
+    call(0)  # 6to4: first sight of the keys (deferred path), untimed
     calls, el, acts = 0, 0.0, 0
     while calls < max(4, args.steps // 50) or el < 1.0:
         np.copyto(mem, orig)
@@ -750,7 +761,7 @@ def bench_nat64_mbufs(args, w):
         acts += int((disp == 0).sum())
         calls += 1
     print(json.dumps({
-        "metric": "end-to-end Mpps, nat64 6to4 over rte_mbuf bursts (" +
+        "metric": f"end-to-end Mpps, nat64 {direction} over rte_mbuf bursts (" +
                   ("cgpu_nat64_frames: (data_address, data_len) pairs, frames rewritten in "
                    "place, data_len left to the caller" if frames else
                    "cgpu_nat64_mbufs: zero-copy gather, rewrite, frames written back into the "
@@ -777,10 +788,11 @@ def e2e_mbufs(args):
 
     torch.cuda.set_device(0)
     w = make_workload(args.config, 0xC0FFEE + 2, n=args.n)
-    if w["kind"] == "nat64" and args.config == "nat64" and args.ingress in ("zero_copy", "frames"):
+    if args.config in ("nat64", "nat64_4to6") and args.ingress in ("zero_copy", "frames"):
         return bench_nat64_mbufs(args, w)
     if w["kind"] != "parse":
-        raise SystemExit("--ingress applies to the parse configs and to nat64 (zero_copy)")
+        raise SystemExit("--ingress applies to the parse configs, and zero_copy / frames to "
+                         "nat64 and nat64_4to6")
     n = len(w["off"])
     ctx = packets.Context(0)
     stride = (128 + 128 + int(w["len"].max()) + 63) // 64 * 64

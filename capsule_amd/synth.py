@@ -444,3 +444,15 @@ def mbuf_frames(mem, mbufs):
     dlen = mem[o + 40].astype(np.uint16) | (mem[o + 41].astype(np.uint16) << np.uint16(8))
     return buf + doff, dlen
 
+
+def mbuf_tailroom(mem, mbufs):
+    """Mbuf::tailroom (core/src/dpdk/mbuf.rs:207-213) of each mbuf of `mem`:
+    buf_len - data_off - data_len, read from its header; the tailroom a
+    4to6 rewrite over (data_address, data_len) pairs needs."""
+    o = (np.asarray(mbufs, dtype=np.uint64) - np.uint64(mem.ctypes.data)).astype(np.int64)
+
+    def u16(at):
+        return mem[at].astype(np.int64) | (mem[at + 1].astype(np.int64) << 8)
+
+    return (u16(o + 54) - u16(o + 16) - u16(o + 40)).astype(np.uint16)
+

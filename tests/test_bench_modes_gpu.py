@@ -60,8 +60,12 @@ def test_bench_e2e(cfg):
 
 @pytest.mark.parametrize("cfg,ingress", [("parse64", "stage"), ("parse64", "zero_copy"),
                                          ("parse64", "frames"), ("imix_csum", "zero_copy"),
-                                         ("nat64", "zero_copy"), ("nat64", "frames")])
+                                         ("nat64", "zero_copy"), ("nat64", "frames"),
+                                         ("nat64_4to6", "zero_copy"), ("nat64_4to6", "frames")])
 def test_bench_e2e_ingress(cfg, ingress):
     d = _run(["--e2e", "--config", cfg, "--ingress", ingress, "--n", N, "--burst", "16384",
               "--steps", "20"])
     assert d["value"] > 0 and d["ingress"] == ingress and d["burst"] == 16384
+    if cfg.startswith("nat64"):  # every frame of the stream (and every reply) is rewritten
+        assert d["act_frac"] == 1.0
+        assert ("4to6" in d["metric"]) == (cfg == "nat64_4to6")
