@@ -164,3 +164,78 @@ def test_oracle_group_by_meta_class_arms():
     idx, off = oracle_lib.group_by(m, 5, N.KEY_META_CLASS)
     assert off.tolist() == [0, 2, 3, 4, 5, 8]
     assert idx.tolist() == [0, 7, 1, 2, 3, 4, 5, 6]
+
+
+def _nat64_6to4_inputs(rng, m):
+    """IPv6 frames for 6to4: the bench's stream shape with UDP drops, VLAN
+    tags, hop limits 0 and 1 (the u8 wrap), truncations at every layer,
+    non-IPv6 frames and frames near the 2048-B data room."""
+    a, o, l = synth.nat64_stream(m, n_keys=m // 8, drop_frac=0.1, seed=int(rng.integers(1 << 30)))
+    frames = [bytes(a[int(s):int(s) + int(n)]) for s, n in zip(o, l)]
+    for vlan in (1, 2):
+        for L in (74 + 4 * vlan, 75 + 4 * vlan, 200, 1500):
+            frames += [bytes(x) for x in synth.build_frames(rng, 20, synth.V6_TCP, L, vlan)]
+    for f in list(frames[:200]):
+        g = bytearray(f)
+        r = rng.random()
+        if r < 0.3:
+            g[21] = int(rng.integers(0, 2))  # hop limit 0 / 1 (no VLAN in the stream)
+        elif r < 0.7:
+            g = g[: int(rng.integers(0, len(g) + 1))]  # truncated anywhere, down to 0 bytes
+        else:
+            g[12:14] = b"\x08\x00"  # not an IPv6 packet
+        frames.append(bytes(g))
+    frames += [bytes(x) for x in synth.build_frames(rng, 5, synth.V6_TCP, 2040, 0)]
+    return frames
+
+
+def test_nat64_oracle_vs_pyref():
+    """The C oracle's nat_6to4 / nat_4to6 against an independent Python
+    restatement (tests/pyref_nat64.py), byte for byte: every disposition,
+    status and ACT frame, NEXT_PORT and the map size, through a 6to4 pass
+    over fuzzed IPv6 frames, a second 6to4 pass (committed keys), and the
+    replies -- with unknown ports, UDP, fragments, truncations, VLAN tags,
+    TTL 0 and frames at the extend tailroom limit -- through 4to6."""
+    import nat64_replies
+    import pyref_nat64
+
+    rng = np.random.default_rng(21)
+    pm = oracle_lib.PortMap()
+    ref = pyref_nat64.Nat64()
+
+    def check(direction, frames, out_off=None, out_size=None):
+        a, o, l = synth.pack_frames(frames)
+        if direction == "6to4":
+            out, olen, disp, st = pm.nat_6to4(a, o, l)
+            oo = o
+        else:
+            out, olen, disp, st = pm.nat_4to6(a, o, l, out_off(o), out_size(a, o))
+            oo = out_off(o)
+        for i, f in enumerate(frames):
+            d, s, g = getattr(ref, "nat_" + direction)(f)
+            assert (int(disp[i]), int(st[i])) == (d, s), (direction, i, len(f))
+            if d == N.ACT:
+                got = bytes(out[int(oo[i]):int(oo[i]) + int(olen[i])])
+                assert got == g, (direction, i)
+        assert pm.next_port() == ref.next_port and pm.size() == len(ref.port_map)
+        return out, o, olen, disp
+
+    frames = _nat64_6to4_inputs(rng, 3000)
+    out, o, olen, disp = check("6to4", frames)
+    check("6to4", frames)  # every key committed now
+    assert {N.ACT, N.DROP, N.ABORT} <= set(disp.tolist())
+    replies = nat64_replies.replies(out, o, olen, disp, rng, junk=0.4)
+    # replies near the tailroom limit (extend(40) needs 40 < tailroom after
+    # shrink(20): frames of 2027 B fit in a 2048-B room, 2028 B do not)
+    base = next(f for f in replies if ref.nat_4to6(f)[0] == N.ACT)
+    for L in (2026, 2027, 2028, 2029):
+        g = bytearray(base + bytes(L - len(base)))
+        k = {0x8100: 1, 0x88A8: 2}.get(int.from_bytes(g[12:14], "big"), 0)
+        g[14 + 4 * k + 2:14 + 4 * k + 4] = (L - 14 - 4 * k).to_bytes(2, "big")
+        replies.append(bytes(g))
+    _, _, _, d4 = check("4to6", replies,
+                        out_off=lambda o: (o + np.arange(len(o), dtype=np.uint64) * 64).astype(np.uint32),
+                        out_size=lambda a, o: len(a) + 64 * len(o) + 64)
+    assert {N.ACT, N.DROP, N.ABORT} <= set(d4.tolist())
+    assert [ref.nat_4to6(f)[:2] for f in replies[-4:]] == [
+        (N.ACT, 0), (N.ACT, 0), (N.ABORT, N.PKT["NOT_RESIZED"]), (N.ABORT, N.PKT["NOT_RESIZED"])]
