@@ -596,8 +596,10 @@ def emit(args, g, m, extra, cpu=None, stub=False):
                    "flow_hash": "bit-exact vs the C oracle; parity unpinned vs the reference "
                                 "(convention: SipHash-1-3(0,0) over Rust-1.50 derive(Hash) "
                                 "of Flow, no reference vector exists)",
-                   "nat64_bytes": "bit-exact vs the C oracle; parity unpinned vs the reference "
-                                  "(examples/nat64 has no test or expected output)"},
+                   "nat64_bytes": "bit-exact vs the C oracle, which a second, independent "
+                                  "restatement (tests/pyref_nat64.py) matches byte for byte; "
+                                  "parity unpinned vs the reference (examples/nat64 has no "
+                                  "test or expected output)"},
     }
     result.update(extra)
     if cpu is not None:
