@@ -96,6 +96,8 @@ def make_workload(cfg, seed, n=1 << 20):
         return dict(arena=arena, off=off, len=ln, flags=0, kind=cfg, desc=desc,
                     out_off=out_off.astype(np.uint32), out_size=int(new_len.sum()) + 64,
                     algo_bytes=int(ln.astype(np.int64).sum()) + 6 * n, frame="256B")
+    if cfg in ("reconcile64", "reconcile_imix"):
+        return reconcile_workload(cfg, seed, n)
     if cfg == "nat64_4to6":
         # the v6 stream that populates the port map; the timed replies are
         # built from its 6to4 output on the device (main())
@@ -105,6 +107,56 @@ def make_workload(cfg, seed, n=1 << 20):
         return dict(arena=arena, off=off, len=ln, flags=0, kind="nat64_4to6", desc=desc,
                     frame="236B")
     raise SystemExit(f"unknown config {cfg}")
+
+
+def reconcile_workload(cfg, seed, n):
+    """Packet::reconcile_all from the L4 layer (packets/mod.rs:297-300) on a
+    parsed burst whose length and checksum fields went stale (a pipeline
+    that rewrote ports, then reconciles before transmit); the parse and the
+    staling are reconcile_setup's (untimed).  Algorithmic bytes: every frame
+    byte (the L4 checksum spans to the frame end) + the 6-B descriptor + the
+    4-B meta word read, plus the fields written (UDP length + checksum, TCP
+    checksum, IPv4 total_length + header checksum, IPv6 payload_length)."""
+    from capsule_amd import _native as N
+    from capsule_amd import synth
+
+    if cfg == "reconcile64":
+        arena, off, ln = synth.uniform(n, seed=seed)
+        flags = N.F_ACCEPT_V4 | N.F_ACCEPT_UDP
+        frame, desc = "64B", f"{_cnt(n)} x 64B Eth/IPv4/UDP"
+    else:
+        arena, off, ln = synth.imix(n, seed=seed)
+        flags = N.F_ACCEPT_ALL
+        frame, desc = "IMIX", f"{_cnt(n)} IMIX 64/570/1500 7:4:1 v4/v6 x UDP/TCP"
+    return dict(arena=arena, off=off, len=ln, flags=flags, kind="reconcile", frame=frame,
+                seed=seed, desc=desc + ": reconcile_all from L4 in place (UDP length + L4 "
+                "checksum, IPv4 total_length + header checksum / IPv6 payload_length) over "
+                "stale fields")
+
+
+def reconcile_setup(w, ctx, dev):
+    """Parse the burst on the device (its meta words, as a pipeline has
+    them), then make its length / checksum fields stale (host side) and set
+    the algorithmic bytes from the layers the parse found.  Returns the
+    device meta tensor; w["arena"] becomes the stale arena."""
+    import torch
+
+    from capsule_amd import _native as N
+    from capsule_amd import packets, synth
+
+    b = packets.PacketBatch.from_numpy(w["arena"], w["off"], w["len"], dev)
+    meta_d = packets.parse(ctx, b, flags=w["flags"]).meta.clone()
+    torch.cuda.synchronize(dev)
+    del b
+    meta = meta_d.cpu().numpy().view(np.uint32)
+    w["arena"] = w["arena"].copy()
+    synth.stale_fields(w["arena"], w["off"], w["len"], meta, seed=w["seed"] + 1)
+    l3, l4 = (meta >> 16) & 3, (meta >> 18) & 3
+    written = np.where(l3 == N.L3_IPV4, 4, 2) + np.where(l4 == N.L4_UDP, 4, 2)
+    n = len(w["off"])
+    w["meta"] = meta
+    w["algo_bytes"] = int(w["len"].astype(np.int64).sum()) + 10 * n + int(written.sum())
+    return meta_d
 
 
 def nat64_4to6_setup(w, ctx, dev):
@@ -186,6 +238,10 @@ def cpu_baseline(w, seconds):
             h = np.zeros(n, np.uint64)
             return lambda: L.or_parse_batch(p(arena), p(off), p(ln), n, w["flags"], p(meta),
                                             p(csum), p(h), None)
+        if w["kind"] == "reconcile":
+            work = arena.copy()
+            meta = w["meta"]
+            return lambda: L.or_reconcile(p(work), p(off), p(ln), p(meta), n, w["flags"], 4, None)
         pm = oracle_lib.PortMap()
         out = np.zeros(len(arena), np.uint8)
         olen = np.zeros(n, np.uint16)
@@ -280,12 +336,13 @@ def cpu_baseline(w, seconds):
 
 
 SEEDS = {"parse64": 2, "parse256": 2, "parse1500": 2, "imix": 3, "imix_csum": 3, "nat64": 4,
-         "nat64_4to6": 4, "nat64_cold": 4}
+         "nat64_4to6": 4, "nat64_cold": 4, "reconcile64": 5, "reconcile_imix": 5}
 CONFIGS = tuple(SEEDS)
 METRIC = "Mpps device-resident parse+cksum+hash @64/256/1500B; % HBM-read roofline"
 # the metric's other sizes and BASELINE's other single-GPU configs, timed in
 # the same N=1 run (the `sizes` object of the line)
-SIZES = ("parse256", "parse1500", "imix", "imix_csum", "nat64", "nat64_4to6", "nat64_cold")
+SIZES = ("parse256", "parse1500", "imix", "imix_csum", "nat64", "nat64_4to6", "nat64_cold",
+         "reconcile64", "reconcile_imix")
 # BASELINE config 5: IMIX shards, one per GPU (the `shards` object)
 SHARD_CONFIG = "imix"
 MIN_WARM_S = 0.15  # device time of warm-up before any timed region (steady clocks)
@@ -331,6 +388,7 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None, queues=1, n_pkts=1 << 
     if w["kind"] == "nat64_cold":
         return bench_nat64_cold(cfg, g, ctx, dev, steps, warmup, w)
     gw = nat64_4to6_setup(w, ctx, dev) if w["kind"] == "nat64_4to6" else None
+    meta_d = reconcile_setup(w, ctx, dev) if w["kind"] == "reconcile" else None
     batch_bytes = len(w["arena"]) + 6 * n
     copies = max(2, -(-2 * INFINITY_CACHE // batch_bytes))
     b0 = packets.PacketBatch.from_numpy(w["arena"], w["off"], w["len"], dev)
@@ -343,6 +401,11 @@ def bench_config(cfg, g, ctx, dev, steps, warmup, w=None, queues=1, n_pkts=1 << 
         outs = [packets.ParseBuffers(n, dev, csum=False) for _ in range(max(2, queues))]
         launchers = [packets.ParseLauncher(ctx, batches[k % copies], outs[k % len(outs)], w["flags"],
                                            streams[k % queues]) for k in range(2 * copies * queues)]
+    elif w["kind"] == "reconcile":
+        assert queues == 1
+        outs = meta_d
+        launchers = [packets.ReconcileLauncher(ctx, batches[k], meta_d, w["flags"], "l4", stream)
+                     for k in range(copies)]
     else:
         assert queues == 1, "one port map, one queue"
         direction = "4to6" if gw is not None else "6to4"

@@ -997,4 +997,34 @@ int cgpu_set_ip(cgpu_ctx *ctx, uint8_t *arena, uint64_t arena_len, const uint32_
   return ok();
 }
 
+int cgpu_reconcile(cgpu_ctx *ctx, uint8_t *arena, uint64_t arena_len, const uint32_t *off,
+                   const uint16_t *len, const uint32_t *meta, uint32_t n, uint32_t flags,
+                   uint32_t depth, uint8_t *status, void *stream) {
+  if (!ctx || n > CGPU_MAX_BATCH) return fail(CGPU_EINVAL);
+  if (depth != CGPU_LAYER_L2 && depth != CGPU_LAYER_L3 && depth != CGPU_LAYER_L4)
+    return fail(CGPU_EINVAL);
+  if (n == 0) return ok();
+  if (!arena || !off || !len || !meta || arena_len > 0xffff0000ull) return fail(CGPU_EINVAL);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
+  // the accept-set defaults of cgpu_parse_batch
+  if ((flags & (CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6)) == 0) flags |= CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6;
+  if ((flags & (CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP | CGPU_F_ACCEPT_ICMP)) == 0)
+    flags |= CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP;
+  cgpu::ParseArgs a{};
+  a.arena = arena;
+  a.arena_len = (uint32_t)arena_len;
+  a.off = off;
+  a.len = len;
+  a.n = n;
+  a.accept = flags & (CGPU_F_ACCEPT_ALL | CGPU_F_ACCEPT_ICMP | CGPU_F_V6_EXT);
+  a.wr_arena = arena;
+  a.meta_in = meta;
+  a.depth = depth;
+  a.rstatus = status;
+  hipError_t e = cgpu::launch_reconcile(a, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e);
+  return ok();
+}
+
 }  // extern "C"

@@ -23,9 +23,18 @@ struct ParseArgs {
   uint64_t *hash;
   cgpu_hdr_record *fields;
   cgpu_ext_record *ext;  // optional, with CGPU_F_V6_EXT
+  // cgpu_reconcile only (the parse kernel's RECON variant): the arena written
+  // in place (= arena), the parse's meta words (read), the layer the packets
+  // are held at and the optional per-packet status
+  uint8_t *wr_arena = nullptr;
+  const uint32_t *meta_in = nullptr;
+  uint32_t depth = 0;
+  uint8_t *rstatus = nullptr;
 };
 
 hipError_t launch_parse(const ParseArgs &a, uint32_t flags, hipStream_t s);
+// Packet::reconcile_all at a.depth (accept set in a.accept).
+hipError_t launch_reconcile(const ParseArgs &a, hipStream_t s);
 
 // ---- nat64 6to4 ------------------------------------------------------------
 // Device port map (examples/nat64/main.rs:37-53): open addressing, linear

@@ -388,7 +388,22 @@ __device__ __forceinline__ void stream_prologue(rsrc_t rs, uint32_t base, uint32
 // parse::<Ipv4>() -> parse::<Udp<Ipv4>>() chain of the reference bench,
 // bench/packets.rs:65-69): every IPv6 / TCP / ICMP branch is compiled out,
 // as Rust monomorphises the typed chain.
-template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT, bool V4U, bool ROWS>
+// A big-endian u16 field store into a frame (any byte offset).
+__device__ __forceinline__ void st16be(uint8_t *p, uint32_t v) {
+  if (((uintptr_t)p & 1u) == 0u) {
+    *reinterpret_cast<uint16_t *>(p) = (uint16_t)swap16(v);
+  } else {
+    p[0] = (uint8_t)(v >> 8);
+    p[1] = (uint8_t)v;
+  }
+}
+
+// RECON: the cgpu_reconcile variant (Packet::reconcile_all, packets/mod.rs:
+// 297-300).  The layers come from the parse's meta words instead of the
+// frame's bytes (a typed packet keeps its parse's offsets), the sums are the
+// parse's, adjusted for the fields reconcile rewrites first (UDP length,
+// IPv4 total_length), and the lane stores the new fields into its frame.
+template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT, bool V4U, bool ROWS, bool RECON = false>
 __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   // No early exit: lanes past n run with len 0 (status BadOffset) and store
@@ -401,6 +416,14 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   const rsrc_t r_len = make_rsrc(a.len, (uint32_t)(2u * nb < 0xffffffffull ? 2u * nb : 0xffffffffull));
   const uint32_t off = __builtin_amdgcn_raw_buffer_load_b32(r_off, (int)(4u * i), 0, 0);
   const uint32_t len = __builtin_amdgcn_raw_buffer_load_b16(r_len, (int)(2u * i), 0, 0);
+  // RECON: the parse's meta word and the layers it records
+  uint32_t mi = 0;
+  if constexpr (RECON) {
+    const rsrc_t r_meta = make_rsrc(a.meta_in, (uint32_t)(4u * nb < 0xffffffffull ? 4u * nb : 0xffffffffull));
+    mi = __builtin_amdgcn_raw_buffer_load_b32(r_meta, (int)(4u * i), 0, 0);
+  }
+  const uint32_t m_k = (mi & CGPU_META_QINQ) ? 2u : ((mi & CGPU_META_DOT1Q) ? 1u : 0u);
+  const uint32_t m_l3 = (mi >> 16) & 3u, m_l4 = (mi >> 18) & 3u, m_x = (mi >> 24) & 3u;
 
   // --- the packet-relative window P ---------------------------------------
   uint32_t P[kWin];
@@ -456,11 +479,13 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     wlim = 64u;
     if (__ballot(len > 64u)) {
       const uint32_t mk = be16_lo(P[3]);
-      const uint32_t kk = mk == 0x8100u ? 1u : (mk == 0x88a8u ? 2u : 0u);
+      const uint32_t kk = RECON ? m_k : (mk == 0x8100u ? 1u : (mk == 0x88a8u ? 2u : 0u));
       const uint32_t et = be16_lo(sel3(kk, P[3], P[4], P[5]));
       const uint32_t w5 = sel3(kk, P[5], P[6], P[7]);  // normalized bytes 20..23
-      const bool is6 = !V4U && et == 0x86ddu;
-      const uint32_t pr = V4U ? 17u : (is6 ? (w5 & 0xffu) : (w5 >> 24));
+      const bool is6 = !V4U && (RECON ? m_l3 == CGPU_L3_IPV6 : et == 0x86ddu);
+      const uint32_t pr = V4U ? 17u
+                          : RECON ? (m_l4 == CGPU_L4_TCP ? 6u : 17u)
+                                  : (is6 ? (w5 & 0xffu) : (w5 >> 24));
       const uint32_t hdr_end = (is6 ? 54u + 4u * kk : 0u) + (pr == 6u ? 20u : 8u);
 #pragma unroll
       for (int c = 4; c < 6; ++c) {
@@ -508,7 +533,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
 
   // --- Ethernet: VLAN marker at bytes 12-13 (ethernet.rs:164-181) ---------
   const uint32_t marker = be16_lo(P[3]);
-  const uint32_t k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
+  const uint32_t k = RECON ? m_k : (marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u));
   const uint32_t eth_len = 14u + 4u * k;  // header_len (ethernet.rs:253-261)
   // Q: the window with the VLAN tags squeezed out (ether_type in Q[3] low
   // half, L3 at normalized byte 14).
@@ -526,14 +551,25 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   const uint32_t ether_type = be16_lo(Q[3]);
 
   // --- status: the first failing step of the reference chain --------------
-  const bool v4 = ether_type == 0x0800u && (a.accept & CGPU_F_ACCEPT_V4);
-  const bool v6 = !V4U && ether_type == 0x86ddu && (a.accept & CGPU_F_ACCEPT_V6);
+  // RECON: the meta's layers, each only if the accept set has it (else the
+  // packet is not one of the pipeline's: NOT_IP / NOT_L4, i.e. skipped)
+  const bool v4 = (RECON ? m_l3 == CGPU_L3_IPV4 : ether_type == 0x0800u) && (a.accept & CGPU_F_ACCEPT_V4);
+  const bool v6 = !V4U && (RECON ? m_l3 == CGPU_L3_IPV6 : ether_type == 0x86ddu) &&
+                  (a.accept & CGPU_F_ACCEPT_V6);
   const uint32_t l3_len = v6 ? 40u : 20u;
-  const uint32_t proto0 = v6 ? (Q[5] & 0xffu) : (Q[5] >> 24);
+  const uint32_t proto0 =
+      !RECON ? (v6 ? (Q[5] & 0xffu) : (Q[5] >> 24))
+      : (EXT && m_x == CGPU_EXT_SRH)      ? 43u
+      : (EXT && m_x == CGPU_EXT_FRAGMENT) ? 44u
+      : m_x != CGPU_EXT_NONE              ? 0x100u  // an extension the accept set lacks
+      : m_l4 == CGPU_L4_UDP               ? 17u
+      : m_l4 == CGPU_L4_TCP               ? 6u
+      : m_l4 == CGPU_L4_ICMP              ? (v6 ? 58u : 1u)
+                                          : 0x100u;
   // --- IPv6 extension header (CGPU_F_V6_EXT): SegmentRouting (43) or
   // Fragment (44) behind IPv6, read per lane from memory (rare: the L4
   // header behind it can lie past the register window) -------------------
-  const bool xcand = EXT && v6 && len > eth_len && eth_len + 40u <= len &&
+  const bool xcand = EXT && (!RECON || L4C) && v6 && len > eth_len && eth_len + 40u <= len &&
                      (proto0 == 43u || proto0 == 44u);
   uint32_t proto = proto0, l4_off = eth_len + l3_len;
   uint32_t xkind = 0u, xst = 0u, xhl = 0u, X0 = 0u, X1 = 0u;
@@ -577,10 +613,18 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       }
     }
   }
-  const bool udp = proto == 17u && (a.accept & CGPU_F_ACCEPT_UDP);
-  const bool tcp = !V4U && proto == 6u && (a.accept & CGPU_F_ACCEPT_TCP);
+  // RECON: the L4 type the meta records (behind an extension header too),
+  // not the next-header byte the frame holds now
+  const uint32_t lp = RECON ? ((mi & 0xffu) != CGPU_PKT_OK || (m_x != CGPU_EXT_NONE && !xok) ? 0x100u
+                               : m_l4 == CGPU_L4_UDP        ? 17u
+                               : m_l4 == CGPU_L4_TCP        ? 6u
+                               : m_l4 == CGPU_L4_ICMP       ? (v6 ? 58u : 1u)
+                                                            : 0x100u)
+                            : proto;
+  const bool udp = lp == 17u && (a.accept & CGPU_F_ACCEPT_UDP);
+  const bool tcp = !V4U && lp == 6u && (a.accept & CGPU_F_ACCEPT_TCP);
   // ProtocolNumbers::Icmpv4 (1) under IPv4, Icmpv6 (58) under IPv6 (ip/mod.rs:41-75)
-  const bool icmp = !V4U && proto == (v6 ? 58u : 1u) && (a.accept & CGPU_F_ACCEPT_ICMP);
+  const bool icmp = !V4U && lp == (v6 ? 58u : 1u) && (a.accept & CGPU_F_ACCEPT_ICMP);
   const uint32_t l4_len = udp ? 8u : (icmp ? 4u : 20u);
   uint32_t st = CGPU_PKT_OK;
   bool eth_ok = false, l3_ok = false;
@@ -616,6 +660,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     }
   }
   const bool l4_ok = st == CGPU_PKT_OK;
+  const uint32_t span16 = (len - l4_off) & 0xffffu;  // Udp/Tcp::len(), the checksum span
 
   uint32_t meta = st;
   if (eth_ok) {
@@ -635,9 +680,11 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
 
   uint32_t ip_c = 0, l4_c = 0;
   if (IPC && l3_ok && !v6) {
-    // compute(0, 20-B header with the checksum zeroed) (v4.rs:322-333)
+    // compute(0, 20-B header with the checksum zeroed) (v4.rs:322-333);
+    // RECON: on the header with total_length := len (v4.rs:486-489)
+    const uint32_t q4 = RECON ? ((Q[4] & 0xffff0000u) | swap16((len - eth_len) & 0xffffu)) : Q[4];
     uint32_t s = sad16(Q[3] & 0xffff0000u, 0u);
-    s = sad16(Q[4], s);
+    s = sad16(q4, s);
     s = sad16(Q[5], s);
     s = sad16(Q[6] & 0xffff0000u, s);
     s = sad16(Q[7], s);
@@ -663,6 +710,8 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
                        : (v6 ? (Q[17] >> 16) : (Q[12] >> 16));
     s -= stored_le;
     if (icmp && !v6) s -= (Q[6] >> 16) + (Q[7] & 0xffffu) + (Q[7] >> 16) + (Q[8] & 0xffffu);
+    // RECON: Udp::reconcile sets length := span before the checksum (udp.rs:350-354)
+    if (RECON && udp) s += swap16(span16) - (v6 ? (Q[14] >> 16) : (Q[9] >> 16));
     has_tail = rows && len > kRowMaxLen;  // the rows summed bytes [0, kRowMaxLen)
     t_b = off + kRowMaxLen;               // 16-B aligned: rows frames are
   }
@@ -689,6 +738,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     // ICMPv4 has no pseudo-header (icmp/v4/mod.rs:118-129): take the
     // addresses (bytes 26..33) back out of the exact sum
     if (icmp && !v6) s -= (Q[6] >> 16) + (Q[7] & 0xffffu) + (Q[7] >> 16) + (Q[8] & 0xffffu);
+    if (RECON && udp) s += swap16(span16) - (v6 ? (Q[14] >> 16) : (Q[9] >> 16));
     has_tail = endn > wq;  // span continues past the window
     t_b = off + 4u * k + wend;  // where it continues (16-B aligned)
     if (xok) {
@@ -715,6 +765,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
       if (off & 1u) r = swap16(r);  // absolute parity -> packet parity (l4_off is even)
       stored_le = udp ? (XU[1] >> 16) : (icmp ? (XU[0] >> 16) : (XU[4] & 0xffffu));
       s = x + r + (0xffffu - stored_le);
+      if (RECON && udp) s += (0xffffu - (XU[1] & 0xffffu)) + swap16(span16);
       has_tail = false;
     }
   }
@@ -991,6 +1042,34 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   }
 
   if (!valid) return;
+  if constexpr (RECON) {
+    // reconcile_all from the held layer outward: L4 (udp.rs:350-354,
+    // tcp.rs:619-621, icmp/v4/mod.rs:246, icmp/v6/mod.rs:260), the
+    // extension header (nothing), then L3 (v4.rs:486-489, v6/mod.rs:331-334)
+    const bool rec = L4C ? l4_ok
+                         : (a.depth >= CGPU_LAYER_L3 ? l3_ok : eth_ok && ((mi >> 8) & 0xffu) != 0u);
+    if (rec) {
+      uint8_t *f = a.wr_arena + off;
+      if (L4C) {
+        if (udp) {
+          st16be(f + l4_off + 4u, span16);
+          st16be(f + l4_off + 6u, l4_c);
+        } else {
+          st16be(f + l4_off + (tcp ? 16u : 2u), l4_c);
+        }
+      }
+      if (a.depth >= CGPU_LAYER_L3) {
+        if (v6) {
+          st16be(f + eth_len + 4u, (len - eth_len - 40u) & 0xffffu);
+        } else {
+          st16be(f + eth_len + 2u, (len - eth_len) & 0xffffu);
+          st16be(f + eth_len + 10u, ip_c);
+        }
+      }
+    }
+    if (a.rstatus != nullptr) a.rstatus[i] = rec ? CGPU_RECON_OK : CGPU_RECON_SKIPPED;
+    return;
+  }
   a.meta[i] = meta;
   if ((IPC || L4C) && a.csum != nullptr) a.csum[i] = ip_c | (l4_c << 16);
 
@@ -1029,7 +1108,33 @@ hipError_t launch_h(const ParseArgs &a, bool hash, bool fields, bool ext, hipStr
   return hash ? launch_f<IPC, L4C, true>(a, fields, ext, s) : launch_f<IPC, L4C, false>(a, fields, ext, s);
 }
 
+template <bool L4C, bool EXT, bool V4U>
+hipError_t launch_recon_t(const ParseArgs &a, hipStream_t s) {
+  const uint32_t grid = (a.n + kBlock - 1) / kBlock;
+  const uint64_t mean = (uint64_t)a.arena_len / a.n;
+  if (L4C && CGPU_PARSE_ROWS && mean >= 128u && mean <= CGPU_PARSE_ROWS_MEAN_MAX)
+    hipLaunchKernelGGL((parse_kernel<true, L4C, false, false, EXT, V4U, true, true>), dim3(grid), dim3(kBlock), 0,
+                       s, a);
+  else
+    hipLaunchKernelGGL((parse_kernel<true, L4C, false, false, EXT, V4U, false, true>), dim3(grid), dim3(kBlock), 0,
+                       s, a);
+  return hipGetLastError();
+}
+
+template <bool L4C>
+hipError_t launch_recon_l(const ParseArgs &a, hipStream_t s) {
+  if (a.accept & CGPU_F_V6_EXT) return launch_recon_t<L4C, true, false>(a, s);
+  constexpr uint32_t kNotV4U = CGPU_F_ACCEPT_V6 | CGPU_F_ACCEPT_TCP | CGPU_F_ACCEPT_ICMP;
+  if (!(a.accept & kNotV4U)) return launch_recon_t<L4C, false, true>(a, s);
+  return launch_recon_t<L4C, false, false>(a, s);
+}
+
 }  // namespace
+
+hipError_t launch_reconcile(const ParseArgs &a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  return a.depth >= CGPU_LAYER_L4 ? launch_recon_l<true>(a, s) : launch_recon_l<false>(a, s);
+}
 
 hipError_t launch_parse(const ParseArgs &a, uint32_t flags, hipStream_t s) {
   if (a.n == 0) return hipSuccess;

@@ -380,6 +380,49 @@ def set_ip(ctx, batch, meta, src=None, dst=None, stream=None, status=None):
     return status
 
 
+_DEPTH = {"l2": N.LAYER_L2, "l3": N.LAYER_L3, "l4": N.LAYER_L4}
+
+
+def reconcile(ctx, batch, meta, flags=None, depth="l4", stream=None, status=None):
+    """`packet.reconcile_all()` (packets/mod.rs:297-300) for every packet of
+    a parsed burst, in place in `batch.arena`, each held at `depth` ("l4",
+    "l3" or "l2") with the layers its parse `meta` recorded: L4 (Udp: length
+    := span, then the checksum, udp.rs:350-354; Tcp / Icmp: the checksum),
+    then L3 (Ipv4: total_length, header checksum, v4.rs:486-489; Ipv6:
+    payload_length, v6/mod.rs:331-334).  `flags`: the accept set the parse
+    ran with.  Returns the per-packet status (RECON_OK / RECON_SKIPPED: the
+    parse did not reach `depth`).  Asynchronous on `stream`."""
+    n = batch.n
+    dev = batch.arena.device
+    if meta.dtype != torch.int32 or meta.numel() != n:
+        raise TypeError("reconcile takes the int32 parse meta tensor of this batch")
+    if flags is None:
+        flags = parse_flags()
+    if status is None:
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
+    rc = N.lib().cgpu_reconcile(ctx.handle, _ptr(batch.arena), batch.arena.numel(), _ptr(batch.off),
+                                _ptr(batch.len), _ptr(meta), n, flags, _DEPTH[depth], _ptr(status),
+                                _stream_handle(stream))
+    N.check(rc, "cgpu_reconcile")
+    return status
+
+
+class ReconcileLauncher:
+    """A `reconcile` call with prebuilt ctypes arguments (bench loops)."""
+
+    def __init__(self, ctx, batch, meta, flags, depth="l4", stream=None, status=None):
+        self._keep = (batch, meta, status)
+        self._fn = N.lib().cgpu_reconcile
+        self._args = [ctx.handle, _ptr(batch.arena), batch.arena.numel(), _ptr(batch.off),
+                      _ptr(batch.len), _ptr(meta), batch.n, flags, _DEPTH[depth], _ptr(status),
+                      _stream_handle(stream)]
+
+    def __call__(self):
+        rc = self._fn(*self._args)
+        if rc:
+            N.check(rc, "cgpu_reconcile")
+
+
 class Nat64Gateway:
     """examples/nat64 6to4 direction with its PORT_MAP on the device.
 

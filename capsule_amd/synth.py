@@ -456,3 +456,44 @@ def mbuf_tailroom(mem, mbufs):
 
     return (u16(o + 54) - u16(o + 16) - u16(o + 40)).astype(np.uint16)
 
+
+
+def stale_fields(arena, off, length, meta, seed=5, frac=1.0):
+    """Make the length and checksum fields that Packet::reconcile_all
+    rewrites stale, in place, on `frac` of the packets whose parse `meta`
+    recorded the layer: random UDP length, L4 checksum, IPv4 total_length and
+    header checksum, IPv6 payload_length, plus a new random destination port
+    (the `set_dst_port` a pipeline makes before reconciling).  Packets behind
+    an IPv6 extension header keep their L4 fields (their L4 offset is not in
+    the meta word).  Returns the number of packets changed."""
+    rng = np.random.default_rng(seed)
+    meta = np.asarray(meta, np.uint32)
+    o = np.asarray(off, np.int64)
+    n = len(o)
+    hit = rng.random(n) < frac
+    hl = ((meta >> 8) & 0xFF).astype(np.int64)
+    l3 = (meta >> 16) & 3
+    l4 = (meta >> 18) & 3
+    ext = (meta >> 24) & 3
+    ok = (meta & 0xFF) == 0
+    ln = np.asarray(length, np.int64)
+
+    def scramble(sel, at):
+        at = at[sel]
+        arena[at] = rng.integers(0, 256, len(at), dtype=np.uint8)
+        arena[at + 1] = rng.integers(0, 256, len(at), dtype=np.uint8)
+
+    v4 = hit & (l3 == 1) & (hl + 20 <= ln)
+    v6 = hit & (l3 == 2) & (hl + 40 <= ln)
+    scramble(v4, o + hl + 2)
+    scramble(v4, o + hl + 10)
+    scramble(v6, o + hl + 4)
+    t = o + hl + np.where(l3 == 2, 40, 20)
+    l4s = hit & ok & (ext == 0) & (l3 != 0)
+    udp, tcp, icmp = l4s & (l4 == 1), l4s & (l4 == 2), l4s & (l4 == 3)
+    scramble(udp, t + 4)
+    scramble(udp, t + 6)
+    scramble(udp | tcp, t + 2)  # set_dst_port
+    scramble(tcp, t + 16)
+    scramble(icmp, t + 2)
+    return int(hit.sum())

@@ -38,8 +38,9 @@ extern "C" {
  *      CGPU_KEY_META_CLASS sends ICMP to the catch-all arm (4); mbufs with
  *      data_off + data_len > buf_len are rejected (CGPU_EINVAL); the mbuf
  *      and frame-pair entry points also check that every byte a frame may
- *      be rewritten into lies in a registered region.                     */
-#define CGPU_ABI_VERSION 3
+ *      be rewritten into lies in a registered region.
+ *   4  cgpu_reconcile (Packet::reconcile_all over a parsed batch).          */
+#define CGPU_ABI_VERSION 4
 
 /* ---- call-level return codes (negative errno style) -------------------- */
 #define CGPU_OK 0
@@ -424,6 +425,45 @@ int cgpu_set_ip(cgpu_ctx *ctx, uint8_t *arena, uint64_t arena_len, const uint32_
                 const uint16_t *len, const uint32_t *meta, uint32_t n, const cgpu_ip_addr *src,
                 uint32_t src_stride, const cgpu_ip_addr *dst, uint32_t dst_stride,
                 uint8_t *status, void *stream);
+
+/* ---- Packet::reconcile_all (core/src/packets/mod.rs:297-300) -------------
+ * The transmit-side fix-up of a header-modifying pipeline, in place, over a
+ * parsed batch (the frames cgpu_parse_batch saw, possibly modified since,
+ * and its meta words; data_len as in `len`).  Every packet is taken as the
+ * typed packet held at layer `depth` -- the layers and offsets its meta
+ * records, as a typed packet keeps the offsets of its parse -- and
+ * reconciled from that layer outward, as reconcile_all walks the envelopes:
+ *   CGPU_LAYER_L4  Udp::reconcile (udp.rs:350-354): length := data_len -
+ *                  offset, then compute_checksum (:204-219) on the frame with
+ *                  that length, 0 stored as 0xFFFF (set_checksum :132-141);
+ *                  Tcp::reconcile (tcp.rs:619-621): compute_checksum;
+ *                  Icmpv4 / Icmpv6::reconcile (icmp/v4/mod.rs:246-248,
+ *                  icmp/v6/mod.rs:260-262): compute_checksum.  Behind an
+ *                  IPv6 extension header (CGPU_F_V6_EXT meta) the
+ *                  pseudo-header is the parse's (segments[0] behind a routing
+ *                  header); SegmentRouting / Fragment reconcile nothing
+ *                  (packets/mod.rs:288).  Then the L3 layer:
+ *   CGPU_LAYER_L3  Ipv4::reconcile (ip/v4.rs:486-489): total_length :=
+ *                  data_len - offset, then the header checksum;
+ *                  Ipv6::reconcile (ip/v6/mod.rs:331-334): payload_length :=
+ *                  data_len - offset - 40.
+ *   CGPU_LAYER_L2  Ethernet: nothing (the default reconcile).
+ * A packet whose parse did not reach `depth` (its meta has no such layer:
+ * the typed parse failed and the reference would hold an Err), or whose
+ * layers no longer fit in data_len, is not touched.  status (optional, u8
+ * per packet) = enum cgpu_recon_status.  flags: the accept set the parse ran
+ * with (CGPU_F_ACCEPT_*, CGPU_F_ACCEPT_ICMP, CGPU_F_V6_EXT, defaults as in
+ * cgpu_parse_batch; other bits are ignored): a packet whose meta records a
+ * layer up to `depth` outside it is SKIPPED, and the set selects the kernel
+ * variant (IPv4/UDP only compiles the other branches out).  Frames must not
+ * overlap.  All device pointers; asynchronous on `stream`.                 */
+#define CGPU_LAYER_L2 2u
+#define CGPU_LAYER_L3 3u
+#define CGPU_LAYER_L4 4u
+enum cgpu_recon_status { CGPU_RECON_OK = 0, CGPU_RECON_SKIPPED = 1 };
+int cgpu_reconcile(cgpu_ctx *ctx, uint8_t *arena, uint64_t arena_len, const uint32_t *off,
+                   const uint16_t *len, const uint32_t *meta, uint32_t n, uint32_t flags,
+                   uint32_t depth, uint8_t *status, void *stream);
 
 /* ---- errors -------------------------------------------------------------- */
 int cgpu_last_error(void);

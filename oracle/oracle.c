@@ -815,6 +815,131 @@ static int or_set_addr(uint8_t *frame, uint32_t l4_off, int udp, int v6, uint32_
   return 0;
 }
 
+/* ---- Packet::reconcile_all (core/src/packets/mod.rs:297-300) --------------
+ * `self.reconcile(); self.envelope_mut().reconcile_all()`: the held layer
+ * first, then every envelope outward.  The layers and their offsets are the
+ * ones the parse recorded in `meta` (a typed packet keeps its offset; the
+ * L4 layer's pseudo-header protocol is its type's constant, udp.rs:212,
+ * tcp.rs:470, icmp/v6/mod.rs:130), the bytes are the frame's current ones. */
+
+/* L4 offset of a packet whose meta records an L4 layer: behind the IPv6
+ * extension header the parse found (SegmentRouting::header_len srh.rs:
+ * 274-276 from the frame's current last_entry, or Fragment's 8 B), with the
+ * parse's checks (srh.rs:299-327); -1 when they fail on the current bytes. */
+static int64_t recon_l4_off(const uint8_t *p, uint32_t len, uint32_t meta, const uint8_t **seg0) {
+  const uint32_t eth = CGPU_META_ETH_LEN(meta), l3 = CGPU_META_L3(meta);
+  uint32_t l4_off = eth + (l3 == CGPU_L3_IPV6 ? 40 : 20);
+  *seg0 = NULL;
+  const uint32_t xk = CGPU_META_EXT(meta);
+  if (xk != CGPU_EXT_NONE) {
+    if (read_data(len, l4_off, 8, 1, 1)) return -1;
+    if (xk == CGPU_EXT_SRH) {
+      const uint8_t *h = p + l4_off;
+      const uint32_t hel = h[1], nseg = (uint32_t)h[4] + 1;
+      if (!(hel != 0 && 2 * nseg == hel)) return -1;
+      if (read_data(len, l4_off + 8, 16 * nseg, 1, 1)) return -1;
+      *seg0 = h + 8;
+      l4_off += 8 + 16 * nseg;
+    } else {
+      l4_off += 8;
+    }
+  }
+  const uint32_t l4 = CGPU_META_L4(meta);
+  const uint32_t l4_len = l4 == CGPU_L4_UDP ? 8 : (l4 == CGPU_L4_TCP ? 20 : 4);
+  if (read_data(len, l4_off, l4_len, 1, 1)) return -1;
+  return l4_off;
+}
+
+/* Udp::reconcile (udp.rs:350-354) / Tcp::reconcile (tcp.rs:619-621) /
+ * Icmpv4::reconcile (icmp/v4/mod.rs:246-248) / Icmpv6 (icmp/v6/mod.rs:260-262) */
+static void l4_reconcile(uint8_t *p, uint32_t len, uint32_t meta, uint32_t l4_off,
+                         const uint8_t *seg0) {
+  const uint32_t eth = CGPU_META_ETH_LEN(meta), l3 = CGPU_META_L3(meta), l4 = CGPU_META_L4(meta);
+  uint8_t *u = p + l4_off;
+  const uint32_t span = len - l4_off; /* self.len(): data_len - offset */
+  if (l4 == CGPU_L4_UDP) wr16(u + 4, (uint16_t)span); /* set_length(len as u16) */
+  const uint32_t cs_at = l4 == CGPU_L4_UDP ? 6 : (l4 == CGPU_L4_TCP ? 16 : 2);
+  wr16(u + cs_at, 0); /* no_checksum / header_mut().checksum = default */
+  const uint8_t pr = l4 == CGPU_L4_UDP ? 17 : (l4 == CGPU_L4_TCP ? 6 : 0x3A);
+  uint16_t ph;
+  if (l4 == CGPU_L4_ICMP && l3 == CGPU_L3_IPV4)
+    ph = 0; /* compute(0, data) (icmp/v4/mod.rs:118-129) */
+  else if (l3 == CGPU_L3_IPV4)
+    ph = or_pseudo_v4(rd32(p + eth + 12), rd32(p + eth + 16), (uint16_t)span, pr);
+  else /* behind a routing header: dst = segments[0] (srh.rs:456-470) */
+    ph = or_pseudo_v6(p + eth + 8, seg0 ? seg0 : p + eth + 24, (uint16_t)span, pr);
+  uint16_t c = or_compute(ph, u, span);
+  if (l4 == CGPU_L4_UDP && c == 0) c = 0xFFFF; /* set_checksum (udp.rs:132-141) */
+  wr16(u + cs_at, c);
+}
+
+/* Ipv4::reconcile (ip/v4.rs:486-489) / Ipv6::reconcile (ip/v6/mod.rs:331-334) */
+static void l3_reconcile(uint8_t *p, uint32_t len, uint32_t meta) {
+  const uint32_t eth = CGPU_META_ETH_LEN(meta);
+  uint8_t *h = p + eth;
+  if (CGPU_META_L3(meta) == CGPU_L3_IPV4) {
+    wr16(h + 2, (uint16_t)(len - eth)); /* set_total_length(self.len() as u16) */
+    wr16(h + 10, 0);                    /* compute_checksum (:322-333) */
+    wr16(h + 10, or_compute(0, h, 20));
+  } else {
+    wr16(h + 4, (uint16_t)(len - eth - 40)); /* set_payload_length(payload_len) */
+  }
+}
+
+/* Whether the accept set (defaults applied as in or_parse_batch_ext) has
+ * every layer meta records up to `depth`. */
+static int recon_accepts(uint32_t flags, uint32_t m, uint32_t depth) {
+  if ((flags & (CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6)) == 0) flags |= CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6;
+  if ((flags & (CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP | CGPU_F_ACCEPT_ICMP)) == 0)
+    flags |= CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP;
+  if (depth >= CGPU_LAYER_L3) {
+    if (CGPU_META_L3(m) == CGPU_L3_IPV4 && !(flags & CGPU_F_ACCEPT_V4)) return 0;
+    if (CGPU_META_L3(m) == CGPU_L3_IPV6 && !(flags & CGPU_F_ACCEPT_V6)) return 0;
+  }
+  if (depth >= CGPU_LAYER_L4) {
+    const uint32_t l4 = CGPU_META_L4(m);
+    if (l4 == CGPU_L4_UDP && !(flags & CGPU_F_ACCEPT_UDP)) return 0;
+    if (l4 == CGPU_L4_TCP && !(flags & CGPU_F_ACCEPT_TCP)) return 0;
+    if (l4 == CGPU_L4_ICMP && !(flags & CGPU_F_ACCEPT_ICMP)) return 0;
+    if (CGPU_META_EXT(m) != CGPU_EXT_NONE && !(flags & CGPU_F_V6_EXT)) return 0;
+  }
+  return 1;
+}
+
+void or_reconcile(uint8_t *arena, const uint32_t *off, const uint16_t *len, const uint32_t *meta,
+                  uint32_t n, uint32_t flags, uint32_t depth, uint8_t *status) {
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t m = meta[i];
+    uint8_t *p = arena + off[i];
+    const uint32_t eth = CGPU_META_ETH_LEN(m);
+    int done = 0;
+    if (!recon_accepts(flags, m, depth)) {
+      /* a layer outside the parse's accept set: not a packet of this pipeline */
+    } else if (depth == CGPU_LAYER_L4) {
+      const uint8_t *seg0;
+      int64_t l4_off = -1;
+      if (CGPU_META_STATUS(m) == CGPU_PKT_OK && CGPU_META_L4(m) != CGPU_L4_NONE &&
+          CGPU_META_L3(m) != CGPU_L3_NONE)
+        l4_off = recon_l4_off(p, len[i], m, &seg0);
+      if (l4_off >= 0) {
+        l4_reconcile(p, len[i], m, (uint32_t)l4_off, seg0);
+        /* SegmentRouting / Fragment: the default reconcile (packets/mod.rs:288) */
+        l3_reconcile(p, len[i], m);
+        done = 1;
+      }
+    } else if (depth == CGPU_LAYER_L3) {
+      if (CGPU_META_L3(m) != CGPU_L3_NONE &&
+          !read_data(len[i], eth, CGPU_META_L3(m) == CGPU_L3_IPV6 ? 40 : 20, 1, 1)) {
+        l3_reconcile(p, len[i], m);
+        done = 1;
+      }
+    } else { /* Ethernet: the default reconcile, nothing */
+      done = eth != 0 && len[i] >= eth;
+    }
+    if (status) status[i] = done ? CGPU_RECON_OK : CGPU_RECON_SKIPPED;
+  }
+}
+
 void or_set_ip(uint8_t *arena, const uint32_t *off, const uint16_t *len, const uint32_t *meta,
                uint32_t n, const cgpu_ip_addr *src, uint32_t src_stride, const cgpu_ip_addr *dst,
                uint32_t dst_stride, uint8_t *status) {

@@ -84,6 +84,11 @@ void or_set_ip(uint8_t *arena, const uint32_t *off, const uint16_t *len, const u
                uint32_t n, const cgpu_ip_addr *src, uint32_t src_stride, const cgpu_ip_addr *dst,
                uint32_t dst_stride, uint8_t *status);
 
+/* Packet::reconcile_all (packets/mod.rs:297-300) at layer `depth` over the
+ * packets of a parsed batch, in place; contract of cgpu_reconcile.        */
+void or_reconcile(uint8_t *arena, const uint32_t *off, const uint16_t *len, const uint32_t *meta,
+                  uint32_t n, uint32_t flags, uint32_t depth, uint8_t *status);
+
 #ifdef __cplusplus
 }
 #endif

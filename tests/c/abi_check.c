@@ -93,6 +93,9 @@ static int (*const p_set_ip)(cgpu_ctx *, uint8_t *, uint64_t, const uint32_t *,
                              const uint16_t *, const uint32_t *, uint32_t, const cgpu_ip_addr *,
                              uint32_t, const cgpu_ip_addr *, uint32_t, uint8_t *,
                              void *) = cgpu_set_ip;
+static int (*const p_reconcile)(cgpu_ctx *, uint8_t *, uint64_t, const uint32_t *,
+                                const uint16_t *, const uint32_t *, uint32_t, uint32_t, uint32_t,
+                                uint8_t *, void *) = cgpu_reconcile;
 static int (*const p_last_error)(void) = cgpu_last_error;
 static const char *(*const p_strerror)(int) = cgpu_strerror;
 static const char *(*const p_pkt_status_str)(int) = cgpu_pkt_status_str;
@@ -107,6 +110,7 @@ static const any_fn entry_points[] = {
     (any_fn)p_set_ip,         (any_fn)p_last_error,       (any_fn)p_strerror,
     (any_fn)p_parse_frames,   (any_fn)p_nat64_frames,
     (any_fn)p_pkt_status_str, (any_fn)p_abi_version,    (any_fn)p_portmap_reset,
+    (any_fn)p_reconcile,
 };
 
 int main(void) {
@@ -117,6 +121,8 @@ int main(void) {
   if (p_abi_version() != CGPU_ABI_VERSION) return 1;
   if (p_parse_batch(NULL, NULL, 0, NULL, NULL) != CGPU_EINVAL) return 2;
   if (p_last_error() != CGPU_EINVAL) return 3;
+  if (p_reconcile(NULL, NULL, 0, NULL, NULL, NULL, 0, 0, CGPU_LAYER_L4, NULL, NULL) != CGPU_EINVAL)
+    return 5;
   printf("abi ok: %zu entry points, %s\n", sizeof entry_points / sizeof entry_points[0],
          p_pkt_status_str(CGPU_PKT_NOT_UDP));
   return 0;

@@ -6,10 +6,10 @@ import numpy as np
 from capsule_amd import _native as N
 
 
-def replies(out, out_off, out_len, disp, rng, junk=0.25):
+def replies(out, out_off, out_len, disp, rng, junk=0.25, max_payload=300):
     """IPv4/TCP reply frames to the 6to4 output frames (dst port = the gateway
     port, so ADDR_MAP hits), plus junk: unknown ports, UDP, fragments,
-    truncations, VLAN tags, TTL 0."""
+    truncations, VLAN tags, TTL 0.  Payloads are 0 .. max_payload - 1 B."""
     import struct
 
     import pyref
@@ -24,7 +24,7 @@ def replies(out, out_off, out_len, disp, rng, junk=0.25):
         vlan = int(rng.integers(0, 3))
         eth = bytes(rng.integers(0, 256, 12, dtype=np.uint8))
         eth += {0: b"", 1: b"\x81\x00\x00\x07", 2: b"\x88\xa8\x00\x01\x81\x00\x00\x02"}[vlan]
-        payload = bytes(rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8))
+        payload = bytes(rng.integers(0, 256, int(rng.integers(0, max_payload)), dtype=np.uint8))
         ttl = int(rng.integers(0, 256))
         proto, flags_frag, gw = 6, 0x4000 if rng.random() < 0.5 else 0, sport
         r = rng.random()

@@ -60,6 +60,8 @@ def load(name="liboracle.so"):
     L.or_nat64_4to6.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
     L.or_set_ip.restype = None
     L.or_set_ip.argtypes = [vp, vp, vp, vp, u32, vp, u32, vp, u32, vp]
+    L.or_reconcile.restype = None
+    L.or_reconcile.argtypes = [vp, vp, vp, vp, u32, u32, u32, vp]
     return L
 
 
@@ -133,6 +135,19 @@ def set_ip(arena, off, length, meta, src=None, dst=None):
     ss = 0 if src is None or len(src) == 1 else 1
     ds = 0 if dst is None or len(dst) == 1 else 1
     lib().or_set_ip(_p(out), _p(off), _p(length), _p(meta), n, _p(src), ss, _p(dst), ds, _p(st))
+    return out, st
+
+
+def reconcile(arena, off, length, meta, flags, depth):
+    """Oracle Packet::reconcile_all at `depth` (3 = L3, 4 = L4) over a parsed
+    batch (arena copied) -> (new arena, status u8[n])."""
+    n = len(off)
+    out = np.array(arena, np.uint8, copy=True)
+    off = np.ascontiguousarray(off, np.uint32)
+    length = np.ascontiguousarray(length, np.uint16)
+    meta = np.ascontiguousarray(meta, np.uint32)
+    st = np.zeros(n, np.uint8)
+    lib().or_reconcile(_p(out), _p(off), _p(length), _p(meta), n, flags, depth, _p(st))
     return out, st
 
 

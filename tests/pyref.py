@@ -149,3 +149,46 @@ def parse(p, flags):
         sport, dport = (p[o] << 8) | p[o + 1], (p[o + 2] << 8) | p[o + 3]
         h = siphash13(flow_bytes(l3 == 2, bytes(src), bytes(dst), sport, dport, pr))
     return 0, meta, ip_c, l4_c, h
+
+
+def reconcile(p, meta, depth):
+    """Packet::reconcile_all (packets/mod.rs:297-300) on one frame, held at
+    `depth` (3 = the IP layer, 4 = the L4 layer) with the layers and offsets
+    its parse `meta` recorded; no extension headers.  -> (bytes, done)."""
+    p = bytearray(p)
+    n = len(p)
+    hl = (meta >> 8) & 0xFF
+    l3, l4 = (meta >> 16) & 3, (meta >> 18) & 3
+    if l3 == 0 or (meta >> 24) & 3:
+        return bytes(p), False
+    l3len = 20 if l3 == 1 else 40
+    if hl + l3len > n:
+        return bytes(p), False
+    o = hl + l3len
+    if depth == 4:
+        if meta & 0xFF or l4 == 0 or o + {1: 8, 2: 20, 3: 4}[l4] > n:
+            return bytes(p), False
+        span = n - o
+        if l4 == 1:  # Udp::reconcile: set_length, then compute_checksum (udp.rs:350-354)
+            p[o + 4:o + 6] = struct.pack(">H", span & 0xFFFF)
+        cs = {1: 6, 2: 16, 3: 2}[l4]
+        p[o + cs:o + cs + 2] = b"\0\0"
+        if l3 == 1:
+            src, dst = p[hl + 12:hl + 16], p[hl + 16:hl + 20]
+        else:
+            src, dst = p[hl + 8:hl + 24], p[hl + 24:hl + 40]
+        pr = {1: 17, 2: 6, 3: 1 if l3 == 1 else 58}[l4]
+        segs = sum(struct.unpack(">%dH" % (len(src) // 2), bytes(src))) + \
+            sum(struct.unpack(">%dH" % (len(dst) // 2), bytes(dst)))
+        ph = 0 if (l4 == 3 and l3 == 1) else fold(segs + pr + (span & 0xFFFF))
+        c = compute(ph, bytes(p[o:]))
+        if l4 == 1 and c == 0:
+            c = 0xFFFF
+        p[o + cs:o + cs + 2] = struct.pack(">H", c)
+    if l3 == 1:  # Ipv4::reconcile (ip/v4.rs:486-489)
+        p[hl + 2:hl + 4] = struct.pack(">H", (n - hl) & 0xFFFF)
+        p[hl + 10:hl + 12] = b"\0\0"
+        p[hl + 10:hl + 12] = struct.pack(">H", compute(0, bytes(p[hl:hl + 20])))
+    else:  # Ipv6::reconcile (ip/v6/mod.rs:331-334)
+        p[hl + 4:hl + 6] = struct.pack(">H", (n - hl - 40) & 0xFFFF)
+    return bytes(p), True

@@ -314,3 +314,53 @@ def test_addr_map_first_mapping_wins(ctx):
         ref = _nat_both(ctx, gw, pm, "4to6", ra, ro, rl, o6, 256 * len(ro) + 64)
         assert (ref[2] == N.ACT).all()
     gw.close()
+
+
+@pytest.mark.parametrize("junk", [0.0, 0.4])
+def test_4to6_rows_path_mixed_waves(ctx, junk):
+    """The 4to6 rows path (input 16-B aligned, output dword-aligned, every
+    frame <= 236 B) on what its waves can hold: VLAN tags (k = 1, 2),
+    mixed lengths, short and truncated frames (partial last chunks), and
+    DROP / ABORT frames among ACT ones.  The same frames with output
+    offsets 2 B off dword alignment take the quad path; both agree with
+    the oracle byte for byte, so with each other."""
+    from capsule_amd import packets
+
+    rng = np.random.default_rng(61)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=14)
+    pm = oracle_lib.PortMap()
+    a, o, l = synth.nat64_stream(8000, n_keys=1200, seed=62)
+    out, olen, disp, _ = _nat_both(ctx, gw, pm, "6to4", a, o, l, o, len(a) + 64)
+    frames = nat64_replies.replies(out, o, olen, disp, rng, junk=junk, max_payload=150)
+    assert max(len(f) for f in frames) <= 236
+    vl = [{0x8100: 1, 0x88A8: 2}.get(int.from_bytes(f[12:14], "big"), 0) for f in frames]
+    assert {0, 1, 2} <= set(vl)
+    ra, ro, rl = synth.pack_frames(frames, slot=64)
+    for shift in (0, 2):  # 0: rows path; 2: every wave falls back to the quad path
+        o6 = (np.arange(len(ro), dtype=np.int64) * 256 + shift).astype(np.uint32)
+        ref = _nat_both(ctx, gw, pm, "4to6", ra, ro, rl, o6, 256 * len(ro) + 64)
+    d = set(ref[2].tolist())
+    assert N.ACT in d and (junk == 0.0 or {N.DROP, N.ABORT} <= d)
+    assert (rl < 64).any() or junk == 0.0
+    gw.close()
+
+
+def test_bench_nat64_4to6_config_every_byte(ctx):
+    """The bench's own 4to6 workload (bench.nat64_4to6_setup): 1 Mi replies
+    in 256-B slots written to the same offsets of the output arena, the map
+    populated by the 6to4 pass over 50,000 keys in a 2^20-slot table, i.e.
+    the rows path the bench times, at its size: every byte, length,
+    disposition and status against the oracle."""
+    import bench
+    from capsule_amd import packets
+
+    w = bench.make_workload("nat64_4to6", 0xC0FFEE + bench.SEEDS["nat64_4to6"])
+    gw = bench.nat64_4to6_setup(w, ctx, torch.device(DEV))
+    pm = oracle_lib.PortMap()
+    pm.nat_6to4(*w["setup"])
+    assert gw.size() == pm.size() and gw.next_port() == pm.next_port()
+    off = w["off"]
+    assert (off % 256 == 0).all() and (w["len"] <= 236).all()
+    ref = _nat_both(ctx, gw, pm, "4to6", w["arena"], off, w["len"], off, len(w["arena"]) + 64)
+    assert (ref[2] == N.ACT).all()
+    gw.close()

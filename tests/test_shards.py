@@ -119,7 +119,7 @@ def test_bench_single_gpu_line_shape():
               "config", "roofline"):
         assert k in d
     assert set(d["sizes"]) == {"parse256", "parse1500", "imix", "imix_csum", "nat64",
-                               "nat64_4to6", "nat64_cold"}
+                               "nat64_4to6", "nat64_cold", "reconcile64", "reconcile_imix"}
     for obj in (d["shards"], d["sizes"]["imix"], d["sizes"]["imix_csum"]):
         assert obj["line_floor_bytes"] > 0 and 0 < obj["frac_of_line_floor"]
     assert d["roofline"]["per_rank"][0]["device"]["pci"] == "stub:00"
