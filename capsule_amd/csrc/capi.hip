@@ -83,7 +83,7 @@ struct cgpu_portmap {
   void *mem;
   // per-call scratch
   uint32_t *pkt_slot = nullptr;
-  uint64_t *lookback = nullptr;
+  uint32_t *chunks = nullptr;
   uint32_t scratch_n = 0;
   uint32_t calls = 0;  // 6to4 calls: parity of the deferred-list counter
   // recorded on the stream of every call that uses the map: calls on one
@@ -735,16 +735,13 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
     if (pm->pkt_slot) (void)hipFree(pm->pkt_slot);
     pm->pkt_slot = nullptr;
     pm->scratch_n = 0;
-    const size_t nb = cgpu::nat64_num_blocks(in->n) + 1;
+    const size_t nb = cgpu::nat64_num_blocks(in->n);
     void *m = nullptr;
-    const size_t o_sums = align_up(4ull * in->n, 256);
-    const size_t o_end = o_sums + align_up(8ull * nb, 256);
-    if (hipMalloc(&m, o_end + 256) != hipSuccess) return fail(CGPU_ENOMEM);
+    const size_t o_chunks = align_up(4ull * in->n, 256);
+    const size_t o_end = o_chunks + align_up(40ull * nb, 256);  // counts, bases, 8-word masks
+    if (hipMalloc(&m, o_end) != hipSuccess) return fail(CGPU_ENOMEM);
     pm->pkt_slot = (uint32_t *)m;
-    pm->lookback = (uint64_t *)((uint8_t *)m + o_sums);
-    // status 0 = "not published" in every epoch
-    if (hipMemsetAsync(pm->lookback, 0, 8ull * nb, (hipStream_t)stream) != hipSuccess)
-      return fail(CGPU_EIO);
+    pm->chunks = (uint32_t *)((uint8_t *)m + o_chunks);
     pm->scratch_n = in->n;
   }
   cgpu::Nat64Args a;
@@ -760,8 +757,7 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   a.disposition = disposition;
   a.status = status;
   a.pkt_slot = pm->pkt_slot;
-  a.lookback = pm->lookback;
-  a.epoch = pm->calls;
+  a.chunks = pm->chunks;
   a.par = pm->calls & 1u;
   a.room = pm->room;
   a.pm = pm->dev;

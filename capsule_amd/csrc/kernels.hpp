@@ -39,17 +39,18 @@ hipError_t launch_reconcile(const ParseArgs &a, hipStream_t s);
 // ---- nat64 6to4 ------------------------------------------------------------
 // Device port map (examples/nat64/main.rs:37-53): open addressing, linear
 // probing over 32-byte slots (PortSlot).  A slot's ref word is 0 (empty),
-// kPersist (committed; its key words are valid) or (packet index + 1) of a
-// representative packet of the batch in flight.
+// kPersist (committed; its key words are valid) or (packet index + 1) of the
+// packet of the batch in flight that claimed it (| kReady once its key words
+// are published).
 constexpr uint32_t kPersist = 0x80000000u;
 
 // One slot of the device port map, 32 bytes (two dwordx4, one cache line
 // half): a lookup is a single line.
-//   w[0] ref   0 empty | kPersist committed | (packet index + 1) batch-local
-//   w[1..4]    key: v6 source address (wire bytes as LE dwords)
-//   w[5]       key: v6-side TCP source port
-//   w[6]       assigned gateway port
-//   w[7]       min packet index of the current batch (0xffffffff idle)
+//   w[0] ref   0 empty | kPersist committed | (claiming packet + 1) [| kReady]
+//   w[1]       claim tag (a second hash of the key; w[0..1] are one 64-bit CAS)
+//   w[2..5]    key: v6 source address (wire bytes as LE dwords)
+//   w[6]       key: v6-side TCP source port | assigned gateway port << 16
+//   w[7]       first packet index of the key in the batch that claimed it
 struct PortSlot {
   uint32_t w[8];
 };
@@ -67,8 +68,8 @@ struct PortMapDev {
   PortSlot *slots;  // [cap]
   u32x4 *rev_addr;     // [65536] (ADDR_MAP: address)
   uint32_t *rev_port;  // [65536] (ADDR_MAP: port | kRevValid)
-  uint32_t *state;  // [11]: next_port, entries, -, -, deferred[2], chunk tickets[2],
-                    // batch new keys, chunks ordered[2]
+  uint32_t *state;  // [16]: next_port, entries, port base, -, then per call parity:
+                    // deferred[2], tail tickets[2], -, phase-1 chunks done[2], phase-2 flag[2]
   uint32_t cap_mask;
 };
 
@@ -84,10 +85,9 @@ struct Nat64Args {
   uint16_t *out_len;
   uint8_t *disposition;
   uint8_t *status;
-  uint32_t *pkt_slot;    // scratch [n]: table slot (or 0xffffffff)
-  uint64_t *lookback;    // scratch [nblocks]: the tail's decoupled look-back words
-  uint32_t epoch;        // 6to4 call number (look-back words of other calls are stale)
-  uint32_t par;          // call parity: selects the per-call counters state[4/6/9 + par]
+  uint32_t *pkt_slot;    // scratch [n]: table slot (| kLocalBit: a key new in this batch), or 0xffffffff
+  uint32_t *chunks;      // scratch [10 nblocks]: the tail's chunk counts, bases, first-packet masks
+  uint32_t par;          // call parity: selects the per-call counters state[4/6/9/11 + par]
   uint32_t room;         // data room of Mbuf::extend's tailroom model (mbuf.rs:225-233):
                          // 2048 for device batches; 65535 on the mbuf path, whose
                          // scatter checks each mbuf's real tailroom instead

@@ -62,7 +62,7 @@ constexpr uint32_t kNow = 4u;                // record info bit: rewrite in the 
 constexpr uint32_t kNoSlot = 0xffffffffu;
 constexpr uint32_t kLocalBit = 0x40000000u;  // pkt_slot: key first seen in this batch
 constexpr uint32_t kSlotMask = 0x3fffffffu;
-constexpr uint32_t kNoPort = 0xffffffffu;       // PortSlot::w[6] of a key not yet ordered
+constexpr uint32_t kReady = 0x40000000u;     // PortSlot ref: the claimer's key words are published
 constexpr uint32_t kV4Addr = 0x017100cbu;    // 203.0.113.1 as LE dword of wire bytes
 // The tailroom model of Mbuf::extend (mbuf.rs:225-233) is Nat64Args::room:
 // RTE_MBUF_DEFAULT_DATAROOM = 2048 for device batches; on the mbuf path the
@@ -93,6 +93,21 @@ __device__ __forceinline__ uint32_t key_hash(const uint32_t (&key)[5]) {
   h ^= h >> 13;
   h *= 0xc2b2ae35u;
   h ^= h >> 16;
+  return h;
+}
+
+// The claim tag: a second, independent hash of the key (a batch-local slot
+// whose tag differs holds another key; an equal tag is confirmed on the key
+// words).
+__device__ __forceinline__ uint32_t key_tag(const uint32_t (&key)[5]) {
+  uint32_t h = 0x2545f491u;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    h = (h ^ key[j]) * 0x9e3779b1u;
+    h ^= h >> 15;
+  }
+  h *= 0x85ebca77u;
+  h ^= h >> 13;
   return h;
 }
 
@@ -247,72 +262,95 @@ __device__ __forceinline__ void ipv4_header(const V6 &v, uint32_t len, uint32_t 
 
 // assigned_port (main.rs:41-53) lookup for frame i: returns the table slot
 // (kNoSlot: table full) and, for a key committed by an earlier batch, its
-// port; a key first seen in this batch is claimed (CAS) or joined, and its
-// first packet index recorded (atomicMin) for the tail kernel.
-__device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, rsrc_t rs, uint32_t i,
+// port; a key first seen in this batch is claimed or joined, and its first
+// packet index recorded (atomicMin) for the tail kernel.
+//
+// A claim is one 64-bit CAS of {ref = i + 1, tag} into an empty slot; the
+// claimer then publishes the key words with write-through (sc1) stores,
+// drains them and sets kReady in ref with an atomic.  A packet that finds a
+// batch-local claim with its own tag waits for kReady (an sc1 poll: the
+// claimer never waits between its CAS and the publish, so the wait ends) and
+// compares the key words, loaded sc1 (MI355X_MICROARCH.md, inter-workgroup
+// visibility: sc1 stores drained before an atomic flag, sc1 poll, sc1
+// loads).  A different tag is a different key: no load, next slot.  Keys
+// committed by earlier batches are matched from the 32-B slot load (their
+// words were written by an earlier launch).  refs only ever go 0 -> (i + 1)
+// -> (i + 1) | kReady -> kPersist, so a stale 0 just leads to the CAS.
+__device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i,
                                                   const uint32_t (&key)[5], uint32_t h, u32x4 s0,
                                                   u32x4 s1, uint32_t &port) {
   port = 0xffffffffu;
+  const uint32_t tag = key_tag(key);
   for (uint32_t probe = 0; probe <= a.pm.cap_mask; ++probe) {
-    // Keys committed by earlier batches are matched from one 32-B slot
-    // load; an empty slot is claimed with a CAS.  refs only ever go
-    // 0 -> (i + 1) -> kPersist, so a stale 0 just leads to the CAS.
     if (probe != 0u) {  // the first slot was loaded by the caller
       const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
       s0 = sp[0];
       s1 = sp[1];
     }
-    uint32_t ref = s0[0];
+    uint32_t *w = a.pm.slots[h].w;
+    uint32_t ref = s0[0], stag = s0[1];
     bool claimed = false;
     if (ref == 0u) {
-      ref = atomicCAS(&a.pm.slots[h].w[0], 0u, i + 1u);
-      claimed = ref == 0u;
+      const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long *>(w), 0ull,
+                                               (unsigned long long)(i + 1u) |
+                                                   ((unsigned long long)tag << 32));
+      claimed = old == 0ull;
+      ref = (uint32_t)old;
+      stag = (uint32_t)(old >> 32);
     }
-    bool match;
+    // Every claimer of the wave publishes before any lane of the wave waits
+    // for a publish (the fences keep the compiler from sinking the publish
+    // below the wait).
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (claimed) {
-      match = true;  // this packet represents the key: publish the key words
 #pragma unroll
-      for (int j = 0; j < 4; ++j) a.pm.slots[h].w[1 + j] = key[j];
-      a.pm.slots[h].w[5] = key[4];
-      a.pm.slots[h].w[6] = kNoPort;  // assigned by the tail kernel's order step
-    } else if (ref & kPersist) {
-      const uint32_t other[5] = {s0[1], s0[2], s0[3], s1[0], s1[1]};
-      match = key_eq(key, other);
-      if (match) port = s1[2];
-    } else {
-      // a key first seen in this batch: compare with the representative
-      // frame's own bytes (immutable input), never with the table words
-      // its claimer may still be writing.
-      const uint32_t rep = ref - 1u;
-      V6 rv;
-      classify(rs, a.arena_len, a.off[rep], a.len[rep], a.room, rv);
-      uint32_t other[5];
-      make_key(rv, other);
-      match = key_eq(key, other);
-    }
-    if (match) {
-      if (ref & kPersist) return h;
-      // the key's first packet index (w[7] only decreases, so a value loaded
-      // with the slot that is already below i makes the atomic moot)
-      if (claimed || s1[3] > i) atomicMin(&a.pm.slots[h].w[7], i);
+      for (int j = 0; j < 5; ++j)
+        __hip_atomic_store(&w[2 + j], key[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0);
+      (void)__hip_atomic_fetch_or(&w[0], kReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicMin(&w[7], i);
       return h | kLocalBit;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (ref & kPersist) {
+      const uint32_t other[5] = {s0[2], s0[3], s1[0], s1[1], s1[2] & 0xffffu};
+      if (key_eq(key, other)) {
+        port = s1[2] >> 16;
+        return h;
+      }
+    } else if (stag == tag) {
+#ifdef CGPU_NAT64_ABL_NOREP  // timing ablation only: tags trusted, no key compare
+      const bool match = true;
+#else
+      while (!(ref & kReady)) {
+        __builtin_amdgcn_s_sleep(1);
+        ref = __hip_atomic_load(&w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      uint32_t other[5];
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        other[j] = __hip_atomic_load(&w[2 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool match = key_eq(key, other);
+#endif
+      if (match) {
+        // the key's first packet index (w[7] only decreases, so a value
+        // loaded with the slot that is already below i makes the atomic moot)
+        if (s1[3] > i) atomicMin(&w[7], i);
+        return h | kLocalBit;
+      }
     }
     h = (h + 1u) & a.pm.cap_mask;
   }
   return kNoSlot;
 }
 
-// assigned_port (main.rs:41-53) lookup for frame i: returns the table slot
-// (kNoSlot: table full) and, for a key committed by an earlier batch, its
-// port; a key first seen in this batch is claimed (CAS) or joined, and its
-// first packet index recorded (atomicMin) for the tail kernel.
-__device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, rsrc_t rs, uint32_t i, const V6 &v,
+__device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, uint32_t i, const V6 &v,
                                                uint32_t &port) {
   uint32_t key[5];
   make_key(v, key);
   const uint32_t h = key_hash(key) & a.pm.cap_mask;
   const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
-  return probe_port_at(a, rs, i, key, h, sp[0], sp[1], port);
+  return probe_port_at(a, i, key, h, sp[0], sp[1], port);
 }
 
 // ---- the rewrite of one frame by its quad (the fused kernel's quad path) -----
@@ -725,7 +763,7 @@ __device__ __forceinline__ void quad_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     slot = 0u;
     port = 1025u;
 #else
-    slot = probe_port(a, rs, d.i, v, port);
+    slot = probe_port(a, d.i, v, port);
 #endif
   }
   slot = qbc<0>(slot);
@@ -984,7 +1022,7 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     slot = 0u;
     port = 1025u;
 #else
-    slot = probe_port_at(a, rs, i, key, h, s0, s1, port);
+    slot = probe_port_at(a, i, key, h, s0, s1, port);
 #endif
   }
   if (v.disp == CGPU_ACT && slot == kNoSlot) {
@@ -1042,169 +1080,173 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a
   for (uint32_t q = 0; q < kRowFrames / 16u; ++q) quad_6to4(a, rs, ors, base + 16u * q + lane / 4u, lane);
 }
 
-// Only packets whose key was first seen in this batch touch the table here.
-__device__ __forceinline__ bool is_first_new(const Nat64Args &a, uint32_t i) {
-  const uint32_t ps = a.pkt_slot[i];
-  if (ps == kNoSlot || !(ps & kLocalBit)) return false;
-  return a.pm.slots[ps & kSlotMask].w[7] == i;
+// ---- the tail kernel: order the batch's new keys, finish their frames ------
+// The batch's keys first seen in it get NEXT_PORT + (rank of their first
+// packet among the first packets of all new keys): AtomicU16::fetch_add in
+// the reference's packet order (main.rs:45-51).  The fused kernel left each
+// such key's first packet index in its slot (w[7], by atomicMin) and each
+// deferred packet's slot in pkt_slot.  One grid takes 2 * nb tickets in
+// order (nb = chunks of kBlock packets):
+//   ticket c < nb        phase 1, chunk c: which of its packets are a new
+//                        key's first packet (pkt_slot local and w[7] == i): a
+//                        256-bit mask and a count per chunk; the workgroup that
+//                        completes phase 1 last scans the counts into each
+//                        chunk's base ordinal, advances NEXT_PORT and raises
+//                        the phase-2 flag;
+//   ticket nb + c        phase 2, chunk c (after the flag): every deferred
+//                        packet computes its key's port from the first
+//                        packet's chunk base and mask -- no hand-off between
+//                        packets of one key -- and patches its frame (the fused
+//                        kernel wrote it with source port 0); a first packet
+//                        also commits the key (port, kPersist, ADDR_MAP).
+// Tickets are taken in order by running workgroups and phase 1 never waits,
+// so the phase-2 wait ends (no co-residency needed).  Data handed between
+// workgroups inside the launch (masks, counts, bases, the port base) is
+// stored sc1, drained before the signalling atomic and loaded sc1
+// (MI355X_MICROARCH.md, inter-workgroup visibility: the last arriver told by
+// its add, a flag polled sc1); everything else was written by an earlier
+// launch.  With nothing deferred (the steady state) the grid exits at once.
+// state: [0] NEXT_PORT [1] entries [2] port base of the batch in flight;
+// by call parity p: [4+p] deferred packets [6+p] tickets [9+p] phase-1
+// chunks done [11+p] phase-2 flag (the other parity is the previous call's,
+// cleared here for the next one).
+__device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
+  return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ---- the tail kernel: order the new keys, patch the deferred frames --------
-// One small persistent grid whose workgroups take 256-packet chunk tickets.
-// For chunk b a workgroup
-//   1. counts the chunk's first packets of new keys, finds their ordinal
-//      base by a decoupled look-back over the earlier chunks' published
-//      counts (each chunk publishes its count, then looks back until it meets
-//      an inclusive prefix), and assigns port = NEXT_PORT + ordinal: the
-//      slot's port word (released), ADDR_MAP, the commit of the key;
-//   2. patches the chunk's deferred frames (the fused kernel rewrote them
-//      with source port 0): the port and the TCP checksum, one thread per
-//      frame, taking each frame's port from its key's slot -- assigned by
-//      this chunk or an earlier one, so a frame may wait for an earlier
-//      chunk's step 1.
-// Every wait is for a lower-numbered chunk, which a running workgroup took
-// (tickets are taken in order by running workgroups), so every wait ends.
-// The workgroup that completes the last chunk advances NEXT_PORT (after
-// every chunk has read it) and clears the next call's counters.
-// Look-back words: epoch << 34 | status << 32 | count (status 1 aggregate,
-// 2 inclusive; a word from an earlier call has another epoch = not yet).
-constexpr uint64_t kLbAgg = 1ull << 32, kLbIncl = 2ull << 32;
-
-__device__ __forceinline__ void reset_next_call(const Nat64Args &a) {
-  a.pm.state[4u + (a.par ^ 1u)] = 0u;  // deferred-list counter
-  a.pm.state[6u + (a.par ^ 1u)] = 0u;  // chunk ticket
-  a.pm.state[9u + (a.par ^ 1u)] = 0u;  // chunks done
-}
-
-__global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_tail(Nat64Args a, uint32_t nb) {
-  __shared__ uint32_t s_chunk, s_prefix;
-  __shared__ uint32_t wcount[kBlock / 64];
-  if (a.pm.state[4u + a.par] == 0u) {  // nothing deferred: no new key
-    if (blockIdx.x == 0 && threadIdx.x == 0) reset_next_call(a);
-    return;
+// The last phase-1 workgroup: exclusive scan of the chunk counts into the
+// chunk bases, the port base, NEXT_PORT advanced (AtomicU16 wrap), the flag.
+__device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const uint32_t *cnt,
+                                          uint32_t *cbase, uint32_t *s_part) {
+  uint32_t *const st = a.pm.state;
+  const uint32_t per = (nb + kBlock - 1u) / kBlock;
+  const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
+  uint32_t sum = 0;
+  for (uint32_t b = b0; b < b1; ++b) sum += ld_sc1(&cnt[b]);
+  s_part[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // 256 partial sums: one thread (the scan of a few thousand counts)
+    uint32_t run = 0;
+    for (uint32_t t = 0; t < kBlock; ++t) {
+      const uint32_t x = s_part[t];
+      s_part[t] = run;
+      run += x;
+    }
+    s_part[kBlock] = run;
   }
+  __syncthreads();
+  uint32_t run = s_part[threadIdx.x];
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t c = ld_sc1(&cnt[b]);
+    st_sc1(&cbase[b], run);
+    run += c;
+  }
+  if (threadIdx.x == 0) {
+    const uint32_t total = s_part[kBlock], base = st[0];
+    st_sc1(&st[2], base);
+    st[0] = (base + total) & 0xffffu;  // read by the next call's launches
+    st[1] += total;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) st_sc1(&st[11u + a.par], 1u);
+}
+
+__global__ __launch_bounds__(kBlock) void nat64_tail(Nat64Args a, uint32_t nb) {
+  __shared__ uint32_t s_ticket, s_last;
+  __shared__ uint32_t s_part[kBlock + 1];
+  uint32_t *const st = a.pm.state;
+  const uint32_t p = a.par;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the previous call's counters, for the next call
+    st[4u + (p ^ 1u)] = 0u;
+    st[6u + (p ^ 1u)] = 0u;
+    st[9u + (p ^ 1u)] = 0u;
+    st[11u + (p ^ 1u)] = 0u;
+  }
+  if (st[4u + p] == 0u) return;  // nothing deferred: no new key
+  uint32_t *const cnt = a.chunks, *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  bool more = true;
-  while (more) {
-    if (threadIdx.x == 0) s_chunk = atomicAdd(&a.pm.state[6u + a.par], 1u);
+  for (;;) {
+    if (threadIdx.x == 0) s_ticket = atomicAdd(&st[6u + p], 1u);
     __syncthreads();
-    const uint32_t b = s_chunk;
-    more = b < nb;  // workgroup-uniform
-    if (more) {
-      // 1. order
-      const uint32_t i = b * kBlock + threadIdx.x;
-      const bool f = i < a.n && is_first_new(a, i);
-      const uint64_t mask = __ballot(f);
-      const uint32_t below = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-      if (lane == 0) wcount[wave] = (uint32_t)__popcll(mask);
-      const uint32_t c = (uint32_t)__syncthreads_count(f);
-      if (wave == 0) {
-        // decoupled look-back by the whole wave: lane l reads chunk
-        // j0 - l's word (64 predecessors per round trip), the nearest
-        // inclusive prefix ends the walk
-        const uint64_t ep = (uint64_t)(a.epoch & 0x3fffffffu) << 34;
-        if (lane == 0)
-          __hip_atomic_store(&a.lookback[b], ep | (b == 0 ? kLbIncl : kLbAgg) | c, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t prefix = 0;
-        for (uint32_t j0 = b; j0 > 0; j0 = j0 > 64u ? j0 - 64u : 0u) {
-          const bool has = lane < j0;
-          const uint32_t j = j0 - 1u - (has ? lane : 0u);
-          uint64_t v = kLbIncl;  // lanes past chunk 0: an empty inclusive prefix
-          if (has) {
-            do {
-              v = __hip_atomic_load(&a.lookback[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } while ((v & ~0x3ffffffffull) != ep || (v & (3ull << 32)) == 0ull);
-          }
-          const uint64_t incl = __ballot(has && (v & kLbIncl));
-          // the nearest inclusive prefix (lowest lane) and the aggregates before it
-          const uint32_t stop = incl ? (uint32_t)__builtin_ctzll(incl) : 63u;
-          uint32_t x = has && lane <= stop ? (uint32_t)v : 0u;
-#pragma unroll
-          for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d);
-          prefix += x;
-          if (incl) break;
-        }
-        if (lane == 0) {
-          if (b != 0)
-            __hip_atomic_store(&a.lookback[b], ep | kLbIncl | (prefix + c), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-          s_prefix = prefix;
-          if (b == nb - 1u)  // the batch's new keys, for the workgroup that finishes last
-            __hip_atomic_store(&a.pm.state[8], prefix + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    const uint32_t t = s_ticket;
+    if (t >= 2u * nb) return;  // workgroup-uniform
+    if (t < nb) {
+      // phase 1: chunk t's first packets of new keys
+      const uint32_t i = t * kBlock + threadIdx.x;
+      const uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
+      const bool f = ps != kNoSlot && (ps & kLocalBit) && a.pm.slots[ps & kSlotMask].w[7] == i;
+      const uint64_t m = __ballot(f);
+      if (lane == 0) {
+        st_sc1(&cmask[8u * t + 2u * wave], (uint32_t)m);
+        st_sc1(&cmask[8u * t + 2u * wave + 1u], (uint32_t)(m >> 32));
       }
+      const uint32_t c = (uint32_t)__syncthreads_count(f);
+      if (threadIdx.x == 0) st_sc1(&cnt[t], c);
+      __builtin_amdgcn_s_waitcnt(0);  // every storing wave drains before the arrival
       __syncthreads();
-      uint32_t pre = s_prefix;
-      for (uint32_t w = 0; w < wave; ++w) pre += wcount[w];
-      uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
-      if (f) {
-        const uint32_t slot = ps & kSlotMask;
-        const uint32_t ordinal = pre + below;
-        const uint32_t port = (a.pm.state[0] + ordinal) & 0xffffu;  // NEXT_PORT.fetch_add order
-        uint32_t key[5];
+      if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(&st[9u + p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1u;
+      __syncthreads();
+      if (s_last) tail_scan(a, nb, cnt, cbase, s_part);
+      __syncthreads();  // s_ticket, s_last, s_part are rewritten next round
+      continue;
+    }
+    // phase 2: chunk t - nb, once every chunk base is known
+    if (threadIdx.x == 0)
+      while (ld_sc1(&st[11u + p]) == 0u) __builtin_amdgcn_s_sleep(2);
+    __syncthreads();
+    const uint32_t i = (t - nb) * kBlock + threadIdx.x;
+    const uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
+    if (ps != kNoSlot && (ps & kLocalBit)) {
+      uint32_t *w = a.pm.slots[ps & kSlotMask].w;
+      const uint32_t fi = w[7];  // the key's first packet
+      const uint32_t fc = fi / kBlock, fb = fi % kBlock;
+      uint32_t below = 0;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) key[j] = a.pm.slots[slot].w[1 + j];
+      for (uint32_t j = 0; j < 8u; ++j) {
+        const uint32_t mw = ld_sc1(&cmask[8u * fc + j]);
+        const uint32_t lo = 32u * j;
+        below += (uint32_t)__builtin_popcount(fb >= lo + 32u ? mw : (fb > lo ? mw & ((1u << (fb - lo)) - 1u) : 0u));
+      }
+      const uint32_t ordinal = ld_sc1(&cbase[fc]) + below;
+      const uint32_t port = (ld_sc1(&st[2]) + ordinal) & 0xffffu;  // NEXT_PORT.fetch_add order
+      if (fi == i) {
+        const u32x4 k0 = *reinterpret_cast<const u32x4 *>(w);      // ref, tag, key[0..1]
+        const u32x4 k1 = *reinterpret_cast<const u32x4 *>(w + 4);  // key[2..4]
         // ADDR_MAP.insert_new(port, key) (main.rs:50): the first mapping of a
         // port wins, also after NEXT_PORT wraps.  This call's ordinals o and
         // o + 65536k share a port, so only its first lap (o < 65536) can be
         // first, and only if no earlier call mapped the port: one writer per
         // entry, no race.
         if (ordinal < 65536u && !(a.pm.rev_port[port] & kRevValid)) {
-          a.pm.rev_addr[port] = u32x4{key[0], key[1], key[2], key[3]};
-          a.pm.rev_port[port] = key[4] | kRevValid;
+          a.pm.rev_addr[port] = u32x4{k0[2], k0[3], k1[0], k1[1]};
+          a.pm.rev_port[port] = (k1[2] & 0xffffu) | kRevValid;
         }
-        // PORT_MAP.insert_new (main.rs:49): commit the key for later batches
-        a.pm.slots[slot].w[7] = 0xffffffffu;
-        a.pm.slots[slot].w[0] = kPersist;
-        // the port itself is all its readers (step 2, any workgroup) use:
-        // a write-through store, no release fence
-        __hip_atomic_store(&a.pm.slots[slot].w[6], port, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // PORT_MAP.insert_new (main.rs:49): the key, committed for later batches
+        w[6] = (k1[2] & 0xffffu) | (port << 16);
+        w[0] = kPersist;
       }
-      // 2. the chunk's deferred frames: the fused kernel wrote them with
-      // source port 0 and the checksum c0 of that frame; set the port and
-      // patch the checksum, ~fold(~c0 + port) -- exact: the sum behind c0
-      // includes the pseudo-header's protocol 6, so it is never 0 and ~c0
-      // recovers its fold.  The port comes from the key's
-      // slot, assigned by this chunk or an earlier one (so a frame may wait
-      // for an earlier chunk's step 1).
-      if (ps != kNoSlot) {
-        const uint32_t slot = ps & kSlotMask;
-        uint32_t port;
-        while ((port = __hip_atomic_load(&a.pm.slots[slot].w[6], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT)) == kNoPort)
-          __builtin_amdgcn_s_sleep(1);
-        uint8_t *o = a.out_arena + a.out_off[i];
-        // the VLAN depth from the output's Ethernet header (the input's own)
-        const uint32_t marker = ((uint32_t)o[12] << 8) | o[13];
-        const uint32_t k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
-        uint8_t *t = o + 34u + 4u * k;  // the TCP header
-        const uint32_t c0 = ((uint32_t)t[16] << 8) | t[17];
-        const uint32_t c = (~fold32(((~c0) & 0xffffu) + port)) & 0xffffu;
-        t[0] = (uint8_t)(port >> 8);
-        t[1] = (uint8_t)port;
-        t[16] = (uint8_t)(c >> 8);
-        t[17] = (uint8_t)c;
-      }
-      // 3. done with chunk b: the last one advances NEXT_PORT
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        // Every read of NEXT_PORT in this chunk is done (the barrier above
-        // waited for them); the write-through store of state[8] is drained
-        // before the count that makes another workgroup read it (no
-        // release / acquire fences: they write back / invalidate the L2).
-        __builtin_amdgcn_s_waitcnt(0);
-        const uint32_t old = __hip_atomic_fetch_add(&a.pm.state[9u + a.par], 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        if (old == nb - 1u) {  // every chunk has read NEXT_PORT: advance it (AtomicU16 wrap)
-          const uint32_t total = __hip_atomic_load(&a.pm.state[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          a.pm.state[0] = (a.pm.state[0] + total) & 0xffffu;
-          a.pm.state[1] += total;
-          reset_next_call(a);
-        }
-      }
+      // The frame was written with source port 0 and the checksum c0 of
+      // that frame; set the port and patch the checksum, ~fold(~c0 + port)
+      // -- exact: the sum behind c0 includes the pseudo-header's protocol 6,
+      // so it is never 0 and ~c0 recovers its fold.
+      uint8_t *o = a.out_arena + a.out_off[i];
+      // the VLAN depth from the output's Ethernet header (the input's own)
+      const uint32_t marker = ((uint32_t)o[12] << 8) | o[13];
+      const uint32_t k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
+      uint8_t *tcp = o + 34u + 4u * k;  // the TCP header
+      const uint32_t c0 = ((uint32_t)tcp[16] << 8) | tcp[17];
+      const uint32_t c = (~fold32(((~c0) & 0xffffu) + port)) & 0xffffu;
+      tcp[0] = (uint8_t)(port >> 8);
+      tcp[1] = (uint8_t)port;
+      tcp[16] = (uint8_t)(c >> 8);
+      tcp[17] = (uint8_t)c;
     }
-    __syncthreads();  // s_chunk, s_prefix, wcount, s_def are rewritten next round
+    __syncthreads();  // s_ticket is rewritten next round
   }
 }
 
@@ -1545,17 +1587,10 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
     pm.rev_port[i] = 0u;
   }
   if (i == 0) {
-    pm.state[0] = first_port;
-    pm.state[1] = 0u;
-    pm.state[2] = 0u;
-    pm.state[3] = 0u;
-    pm.state[4] = 0u;  // deferred-list counters, by call parity
-    pm.state[5] = 0u;
-    pm.state[6] = 0u;  // look-back chunk tickets, by call parity
-    pm.state[7] = 0u;
-    pm.state[8] = 0u;  // new keys of the last batch
-    pm.state[9] = 0u;  // chunks ordered, by call parity
-    pm.state[10] = 0u;
+    pm.state[0] = first_port;  // NEXT_PORT
+    // entries, the port base, and the per-call-parity counters of the tail
+    // (deferred packets, tickets, phase-1 chunks done, phase-2 flag)
+    for (uint32_t j = 1; j < 16u; ++j) pm.state[j] = 0u;
   }
 }
 
@@ -1564,9 +1599,9 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
 uint32_t nat64_num_blocks(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 
 #ifndef CGPU_NAT64_TAIL_GRID
-#define CGPU_NAT64_TAIL_GRID 1024
+#define CGPU_NAT64_TAIL_GRID 2048
 #endif
-constexpr uint32_t kTailGrid = CGPU_NAT64_TAIL_GRID;  // workgroups of the tail kernel
+constexpr uint32_t kTailGrid = CGPU_NAT64_TAIL_GRID;  // most workgroups of the tail kernel
 
 hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStream_t s) {
   // one thread per slot and ADDR_MAP entry
@@ -1581,9 +1616,10 @@ hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s) {
   const uint32_t fpb = (kBlock / 64u) * kRowFrames;  // fused: kRowFrames frames per wave
   const uint32_t nbf = (a.n + fpb - 1) / fpb;
   hipLaunchKernelGGL(nat64_6to4_fused, dim3(nbf), dim3(kBlock), 0, s, a);
-  // the tail (order + deferred rewrite) is one small persistent grid; in the
+  // the tail (order + the deferred frames' ports) takes 2 nb tickets; in the
   // steady state (no new key) it returns at once
-  hipLaunchKernelGGL(nat64_tail, dim3(kTailGrid), dim3(kBlock), 0, s, a, nb);
+  const uint32_t tg = 2u * nb < kTailGrid ? 2u * nb : kTailGrid;
+  hipLaunchKernelGGL(nat64_tail, dim3(tg), dim3(kBlock), 0, s, a, nb);
   return hipGetLastError();
 }
 

@@ -7,5 +7,6 @@ step nat64_new 600 python -u -m pytest tests/test_nat64_gpu.py -x -v --timeout 3
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_recon64 300 python bench.py --config reconcile64 --only --no-cpu --steps 300
 step bench_recon_imix 300 python bench.py --config reconcile_imix --only --no-cpu --steps 300
+step launch_gap 120 tools/launch_gap
 bash scripts/profile.sh r4_reconcile64 --config reconcile64 --steps 100 || exit $?
 bash scripts/profile.sh r4_reconcile_imix --config reconcile_imix --steps 100 || exit $?

@@ -1,0 +1,114 @@
+// launch_gap.hip — what a kernel that finds nothing to do costs on the
+// stream timeline, and what a per-call hipEventRecord costs, behind a real
+// HBM-streaming kernel (the nat64 tail design question: how many "exit at
+// once" launches may follow the fused kernel in the steady state).
+//
+// Per iteration: one streaming kernel (reads 256 MiB, ~45 us), then m empty
+// kernels of g workgroups (each reads one flag word and returns), optionally
+// a hipEventRecord.  Mean device time per iteration from events around 200
+// back-to-back iterations, minus the m = 0 case.
+//   build: hipcc -O3 --offload-arch=gfx950 tools/launch_gap.hip -o tools/launch_gap
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CK(x)                                                                 \
+  do {                                                                        \
+    hipError_t e_ = (x);                                                      \
+    if (e_ != hipSuccess) {                                                   \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(2);                                                                \
+    }                                                                         \
+  } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void stream(const u32x4 *p, size_t n16, uint32_t *out) {
+  uint32_t acc = 0;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256ull) {
+    u32x4 v = p[i];
+    acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+  }
+  if (acc == 0x9e3779b9u) out[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(256) void empty(const uint32_t *flag, uint32_t *out) {
+  if (*flag == 0u) return;  // the steady state: nothing deferred
+  out[blockIdx.x * 256 + threadIdx.x] = 1u;
+}
+
+int main() {
+  const size_t bytes = 256ull << 20;
+  u32x4 *buf;
+  uint32_t *flag, *out;
+  CK(hipMalloc(&buf, bytes));
+  CK(hipMemset(buf, 1, bytes));
+  CK(hipMalloc(&flag, 4));
+  CK(hipMemset(flag, 0, 4));
+  CK(hipMalloc(&out, 4 << 20));
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t a, b, rec;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  CK(hipEventCreateWithFlags(&rec, hipEventDisableTiming));
+  const int iters = 200;
+  double base = 0;
+  const int grids[] = {1, 64, 256, 1024};
+  for (int ev = 0; ev < 2; ++ev) {
+    for (int gi = 0; gi < 4; ++gi) {
+      for (int m = 0; m <= 4; ++m) {
+        if (m == 0 && gi > 0) continue;
+        for (int rep = 0; rep < 2; ++rep) {  // rep 0 warms up
+          CK(hipEventRecord(a, s));
+          for (int it = 0; it < iters; ++it) {
+            hipLaunchKernelGGL(stream, dim3(2048), dim3(256), 0, s, buf, bytes / 16, out);
+            for (int k = 0; k < m; ++k)
+              hipLaunchKernelGGL(empty, dim3(grids[gi]), dim3(256), 0, s, flag, out);
+            if (ev) CK(hipEventRecord(rec, s));
+          }
+          CK(hipEventRecord(b, s));
+          CK(hipEventSynchronize(b));
+          float ms;
+          CK(hipEventElapsedTime(&ms, a, b));
+          const double us = ms * 1e3 / iters;
+          if (rep == 1) {
+            if (m == 0 && ev == 0) base = us;
+            printf("event_record=%d grid=%4d empty_kernels=%d  us/iter=%8.2f  extra=%7.2f\n", ev,
+                   m ? grids[gi] : 0, m, us, us - base);
+          }
+        }
+      }
+    }
+  }
+  // the ways a call can leave a completion marker / order itself after the
+  // previous call (the nat64 port map's cross-call ordering)
+  hipEvent_t rec_t;
+  CK(hipEventCreate(&rec_t));
+  const char *names[] = {"ext_launch stop event (no timing flag)", "ext_launch stop event (timing)",
+                         "event_record + wait_event same stream", "wait_event only (old event)"};
+  for (int mode = 0; mode < 4; ++mode) {
+    for (int rep = 0; rep < 2; ++rep) {
+      CK(hipEventRecord(a, s));
+      for (int it = 0; it < iters; ++it) {
+        if (mode == 0)
+          hipExtLaunchKernelGGL(stream, dim3(2048), dim3(256), 0, s, nullptr, rec, 0, buf, bytes / 16, out);
+        else if (mode == 1)
+          hipExtLaunchKernelGGL(stream, dim3(2048), dim3(256), 0, s, nullptr, rec_t, 0, buf, bytes / 16, out);
+        else
+          hipLaunchKernelGGL(stream, dim3(2048), dim3(256), 0, s, buf, bytes / 16, out);
+        if (mode == 2) CK(hipEventRecord(rec, s));
+        if (mode >= 2) CK(hipStreamWaitEvent(s, rec, 0));
+      }
+      CK(hipEventRecord(b, s));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      const double us = ms * 1e3 / iters;
+      if (rep == 1) printf("%-42s us/iter=%8.2f  extra=%7.2f\n", names[mode], us, us - base);
+    }
+  }
+  return 0;
+}
