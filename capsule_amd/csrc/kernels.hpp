@@ -68,8 +68,9 @@ struct PortMapDev {
   PortSlot *slots;  // [cap]
   u32x4 *rev_addr;     // [65536] (ADDR_MAP: address)
   uint32_t *rev_port;  // [65536] (ADDR_MAP: port | kRevValid)
-  uint32_t *state;  // [16]: next_port, entries, port base, -, then per call parity:
-                    // deferred[2], tail tickets[2], -, phase-1 chunks done[2], phase-2 flag[2]
+  uint32_t *state;  // [64]: line 0: next_port, entries, -, -, then per call parity:
+                    // deferred[2], tail tickets[2], -, phase-1 chunks done[2];
+                    // line 1 (words 32..): the tail's port base and phase-2 flags[2]
   uint32_t cap_mask;
 };
 

@@ -266,16 +266,30 @@ __device__ __forceinline__ void ipv4_header(const V6 &v, uint32_t len, uint32_t 
 // packet index recorded (atomicMin) for the tail kernel.
 //
 // A claim is one 64-bit CAS of {ref = i + 1, tag} into an empty slot; the
-// claimer then publishes the key words with write-through (sc1) stores,
-// drains them and sets kReady in ref with an atomic.  A packet that finds a
-// batch-local claim with its own tag waits for kReady (an sc1 poll: the
-// claimer never waits between its CAS and the publish, so the wait ends) and
-// compares the key words, loaded sc1 (MI355X_MICROARCH.md, inter-workgroup
-// visibility: sc1 stores drained before an atomic flag, sc1 poll, sc1
-// loads).  A different tag is a different key: no load, next slot.  Keys
-// committed by earlier batches are matched from the 32-B slot load (their
-// words were written by an earlier launch).  refs only ever go 0 -> (i + 1)
-// -> (i + 1) | kReady -> kPersist, so a stale 0 just leads to the CAS.
+// claimer then publishes the key words with atomic exchanges and, once they
+// have returned, sets kReady in ref with an atomic OR.  A packet that finds
+// a batch-local claim with its own tag waits for kReady and compares the
+// key words, both read with atomic RMWs (an OR of 0): atomics are performed
+// at the memory-side coherence point, so no XCD's L2 can serve them a stale
+// copy of the slot line (its own earlier probe load cached one: plain or
+// sc1 reads of the words published in this launch would read it,
+// MI355X_MICROARCH.md, inter-workgroup visibility).  The claimer never waits
+// between its CAS and the publish, so the wait ends.  A different tag is a
+// different key: no read, next slot.  Keys committed by earlier batches are
+// matched from the 32-B slot load (their words were written by an earlier
+// launch).  refs only ever go 0 -> (i + 1) -> (i + 1) | kReady -> kPersist,
+// and a claim's tag never changes, so a stale probe load at worst leads to
+// the CAS, which returns the coherent word.
+// (An idempotent OR / ADD would be compiled into an sc1 load, which the L2
+// serves; a compare-exchange of 0 with 0 is performed at the coherence point
+// and leaves the word as it is.)
+__device__ __forceinline__ uint32_t rd_atomic(uint32_t *p) {
+  return atomicCAS(p, 0u, 0u);
+}
+__device__ __forceinline__ uint64_t rd_atomic64(uint32_t *p) {
+  return atomicCAS(reinterpret_cast<unsigned long long *>(p), 0ull, 0ull);
+}
+
 __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i,
                                                   const uint32_t (&key)[5], uint32_t h, u32x4 s0,
                                                   u32x4 s1, uint32_t &port) {
@@ -305,8 +319,9 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
     if (claimed) {
 #pragma unroll
       for (int j = 0; j < 5; ++j)
-        __hip_atomic_store(&w[2 + j], key[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_waitcnt(0);
+        (void)__hip_atomic_exchange(&w[2 + j], key[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the exchanges are performed before the flag
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       (void)__hip_atomic_fetch_or(&w[0], kReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       atomicMin(&w[7], i);
       return h | kLocalBit;
@@ -322,14 +337,13 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
 #ifdef CGPU_NAT64_ABL_NOREP  // timing ablation only: tags trusted, no key compare
       const bool match = true;
 #else
-      while (!(ref & kReady)) {
+      for (uint32_t spin = 0; !(ref & kReady) && spin < (1u << 22); ++spin) {
         __builtin_amdgcn_s_sleep(1);
-        ref = __hip_atomic_load(&w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ref = rd_atomic(&w[0]);
       }
-      uint32_t other[5];
-#pragma unroll
-      for (int j = 0; j < 5; ++j)
-        other[j] = __hip_atomic_load(&w[2 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t k01 = rd_atomic64(&w[2]), k23 = rd_atomic64(&w[4]);
+      const uint32_t other[5] = {(uint32_t)k01, (uint32_t)(k01 >> 32), (uint32_t)k23,
+                                 (uint32_t)(k23 >> 32), rd_atomic(&w[6])};
       const bool match = key_eq(key, other);
 #endif
       if (match) {
@@ -1106,16 +1120,19 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a
 // (MI355X_MICROARCH.md, inter-workgroup visibility: the last arriver told by
 // its add, a flag polled sc1); everything else was written by an earlier
 // launch.  With nothing deferred (the steady state) the grid exits at once.
-// state: [0] NEXT_PORT [1] entries [2] port base of the batch in flight;
-// by call parity p: [4+p] deferred packets [6+p] tickets [9+p] phase-1
-// chunks done [11+p] phase-2 flag (the other parity is the previous call's,
-// cleared here for the next one).
+// state (128-B line 0): [0] NEXT_PORT [1] entries; by call parity p:
+// [4+p] deferred packets [6+p] tickets [9+p] phase-1 chunks done (the other
+// parity is the previous call's, cleared here for the next one).  The words
+// handed over inside the launch sit on line 1, which nothing reads with a
+// plain load (every workgroup reads line 0 plainly, so its L2 holds it):
+// [32] the port base of the batch in flight, [33+p] the phase-2 flag.
 __device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
   return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+constexpr uint32_t kStBase = 32u, kStFlag = 33u;  // state line 1
 
 // The last phase-1 workgroup: exclusive scan of the chunk counts into the
 // chunk bases, the port base, NEXT_PORT advanced (AtomicU16 wrap), the flag.
@@ -1146,13 +1163,13 @@ __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const
   }
   if (threadIdx.x == 0) {
     const uint32_t total = s_part[kBlock], base = st[0];
-    st_sc1(&st[2], base);
+    st_sc1(&st[kStBase], base);
     st[0] = (base + total) & 0xffffu;  // read by the next call's launches
     st[1] += total;
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (threadIdx.x == 0) st_sc1(&st[11u + a.par], 1u);
+  if (threadIdx.x == 0) st_sc1(&st[kStFlag + a.par], 1u);
 }
 
 __global__ __launch_bounds__(kBlock) void nat64_tail(Nat64Args a, uint32_t nb) {
@@ -1164,7 +1181,7 @@ __global__ __launch_bounds__(kBlock) void nat64_tail(Nat64Args a, uint32_t nb) {
     st[4u + (p ^ 1u)] = 0u;
     st[6u + (p ^ 1u)] = 0u;
     st[9u + (p ^ 1u)] = 0u;
-    st[11u + (p ^ 1u)] = 0u;
+    st[kStFlag + (p ^ 1u)] = 0u;
   }
   if (st[4u + p] == 0u) return;  // nothing deferred: no new key
   uint32_t *const cnt = a.chunks, *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
@@ -1195,10 +1212,14 @@ __global__ __launch_bounds__(kBlock) void nat64_tail(Nat64Args a, uint32_t nb) {
       __syncthreads();  // s_ticket, s_last, s_part are rewritten next round
       continue;
     }
-    // phase 2: chunk t - nb, once every chunk base is known
-    if (threadIdx.x == 0)
-      while (ld_sc1(&st[11u + p]) == 0u) __builtin_amdgcn_s_sleep(2);
+    // phase 2: chunk t - nb, once every chunk base is known (the flag is
+    // polled with a compare-exchange, performed at the coherence point)
+    if (threadIdx.x == 0) {
+      while (atomicCAS(&st[kStFlag + p], 0u, 0u) == 0u) __builtin_amdgcn_s_sleep(2);
+      s_last = ld_sc1(&st[kStBase]);
+    }
     __syncthreads();
+    const uint32_t port_base = s_last;
     const uint32_t i = (t - nb) * kBlock + threadIdx.x;
     const uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
     if (ps != kNoSlot && (ps & kLocalBit)) {
@@ -1213,7 +1234,7 @@ __global__ __launch_bounds__(kBlock) void nat64_tail(Nat64Args a, uint32_t nb) {
         below += (uint32_t)__builtin_popcount(fb >= lo + 32u ? mw : (fb > lo ? mw & ((1u << (fb - lo)) - 1u) : 0u));
       }
       const uint32_t ordinal = ld_sc1(&cbase[fc]) + below;
-      const uint32_t port = (ld_sc1(&st[2]) + ordinal) & 0xffffu;  // NEXT_PORT.fetch_add order
+      const uint32_t port = (port_base + ordinal) & 0xffffu;  // NEXT_PORT.fetch_add order
       if (fi == i) {
         const u32x4 k0 = *reinterpret_cast<const u32x4 *>(w);      // ref, tag, key[0..1]
         const u32x4 k1 = *reinterpret_cast<const u32x4 *>(w + 4);  // key[2..4]
@@ -1590,7 +1611,7 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
     pm.state[0] = first_port;  // NEXT_PORT
     // entries, the port base, and the per-call-parity counters of the tail
     // (deferred packets, tickets, phase-1 chunks done, phase-2 flag)
-    for (uint32_t j = 1; j < 16u; ++j) pm.state[j] = 0u;
+    for (uint32_t j = 1; j < 64u; ++j) pm.state[j] = 0u;
   }
 }
 

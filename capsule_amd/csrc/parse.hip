@@ -63,6 +63,9 @@ constexpr uint32_t kSlotIt = CGPU_SLOT_IT;  // slots per 16-lane row and round (
 #define CGPU_PARSE_ROW_MAX 512
 #endif
 constexpr uint32_t kRowMaxLen = CGPU_PARSE_ROW_MAX;  // the rows path: frames up to 2 pieces
+#ifndef CGPU_RECON_WHOLE  // reconcile: rewrite a frame's first 64 B whole (0: field stores only)
+#define CGPU_RECON_WHOLE 1
+#endif
 
 __device__ __forceinline__ uint32_t sel3(uint32_t k, uint32_t a, uint32_t b, uint32_t c) {
   return k == 0u ? a : (k == 1u ? b : c);
@@ -1049,22 +1052,66 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     const bool rec = L4C ? l4_ok
                          : (a.depth >= CGPU_LAYER_L3 ? l3_ok : eth_ok && ((mi >> 8) & 0xffu) != 0u);
     if (rec) {
-      uint8_t *f = a.wr_arena + off;
+      // the fields reconcile writes: frame position and big-endian value
+      uint32_t fp[4], fv[4], nf = 0;
       if (L4C) {
         if (udp) {
-          st16be(f + l4_off + 4u, span16);
-          st16be(f + l4_off + 6u, l4_c);
+          fp[0] = l4_off + 4u;
+          fv[0] = span16;
+          fp[1] = l4_off + 6u;
+          fv[1] = l4_c;
+          nf = 2;
         } else {
-          st16be(f + l4_off + (tcp ? 16u : 2u), l4_c);
+          fp[0] = l4_off + (tcp ? 16u : 2u);
+          fv[0] = l4_c;
+          nf = 1;
         }
       }
       if (a.depth >= CGPU_LAYER_L3) {
         if (v6) {
-          st16be(f + eth_len + 4u, (len - eth_len - 40u) & 0xffffu);
+          fp[nf] = eth_len + 4u;
+          fv[nf++] = (len - eth_len - 40u) & 0xffffu;
         } else {
-          st16be(f + eth_len + 2u, (len - eth_len) & 0xffffu);
-          st16be(f + eth_len + 10u, ip_c);
+          fp[nf] = eth_len + 2u;
+          fv[nf++] = (len - eth_len) & 0xffffu;
+          fp[nf] = eth_len + 10u;
+          fv[nf++] = ip_c;
         }
+      }
+      uint8_t *f = a.wr_arena + off;
+#if CGPU_RECON_WHOLE
+      // A dword-aligned frame of 64 B or more gets its first 64 bytes back
+      // whole (the window with the fields patched in: whole 16-B chunks, a
+      // fully written 64-B sector for frames in 64-B slots) instead of 2-B
+      // stores into partly written sectors; fields past byte 64 (IPv6 behind
+      // tags / TCP) are stored alone.
+      if ((off & 3u) == 0u && len >= 64u) {
+        uint32_t W[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) W[j] = P[j];
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; ++q) {
+          if (q >= nf) break;
+          const uint32_t pos = fp[q], v = swap16(fv[q]);
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            if ((pos >> 2) == (uint32_t)j)
+              W[j] = (pos & 2u) ? ((W[j] & 0xffffu) | (v << 16)) : ((W[j] & 0xffff0000u) | v);
+        }
+        const rsrc_t ws = make_rsrc(a.wr_arena, a.arena_len);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{W[4 * c], W[4 * c + 1], W[4 * c + 2], W[4 * c + 3]}, ws,
+                                                 (int)(off + 16u * c), 0, 0);
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; ++q)
+          if (q < nf && fp[q] >= 64u) st16be(f + fp[q], fv[q]);
+      } else
+#endif
+      {
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; ++q)
+          if (q < nf) st16be(f + fp[q], fv[q]);
       }
     }
     if (a.rstatus != nullptr) a.rstatus[i] = rec ? CGPU_RECON_OK : CGPU_RECON_SKIPPED;

@@ -364,3 +364,64 @@ def test_bench_nat64_4to6_config_every_byte(ctx):
     ref = _nat_both(ctx, gw, pm, "4to6", w["arena"], off, w["len"], off, len(w["arena"]) + 64)
     assert (ref[2] == N.ACT).all()
     gw.close()
+
+
+class _RawStream:
+    """A HIP stream of our own (hipStreamCreate / hipStreamDestroy through
+    libamdhip64), usable where the packets API takes a torch stream."""
+
+    def __init__(self):
+        import ctypes
+
+        self._hip = ctypes.CDLL("libamdhip64.so")
+        self._h = ctypes.c_void_p()
+        assert self._hip.hipStreamCreate(ctypes.byref(self._h)) == 0
+        self.cuda_stream = self._h.value
+
+    def destroy(self):
+        assert self._hip.hipStreamDestroy(self._h) == 0
+
+
+def test_portmap_calls_ordered_across_streams(ctx):
+    """include/capsule_gpu.h: calls on one map are ordered even on different
+    streams, and next_port()/size() wait for the map's latest call after its
+    stream is gone.  6to4 on stream A, reset on stream B, 6to4 on A, 4to6 on
+    B, no host sync in between; B destroyed before the state reads.  Every
+    output and the map state equal the oracle's (a fresh map after the
+    reset)."""
+    from capsule_amd import packets
+
+    a1, o1, l1 = synth.nat64_stream(12_000, n_keys=2000, seed=71)
+    a2, o2, l2 = synth.nat64_stream(12_000, n_keys=2500, seed=72)
+    pm1, pm2 = oracle_lib.PortMap(), oracle_lib.PortMap()
+    want1 = pm1.nat_6to4(a1, o1, l1)
+    want2 = pm2.nat_6to4(a2, o2, l2)
+    keep = np.nonzero(want2[2] == N.ACT)[0]
+    ra, ro, rl = synth.nat64_replies(want2[0], o2[keep], want2[1][keep])
+    o6 = (np.arange(len(ro), dtype=np.int64) * 256).astype(np.uint32)
+    want3 = pm2.nat_4to6(ra, ro, rl, o6, 256 * len(ro) + 64)
+
+    gw = packets.Nat64Gateway(ctx, capacity_log2=16)
+    b1 = packets.PacketBatch.from_numpy(a1, o1, l1, DEV)
+    b2 = packets.PacketBatch.from_numpy(a2, o2, l2, DEV)
+    b3 = packets.PacketBatch.from_numpy(ra, ro, rl, DEV)
+    out1 = torch.zeros(len(a1), dtype=torch.uint8, device=DEV)
+    out2 = torch.zeros(len(a2), dtype=torch.uint8, device=DEV)
+    out3 = torch.zeros(256 * len(ro) + 64, dtype=torch.uint8, device=DEV)
+    oo6 = torch.from_numpy(o6.view(np.int32)).to(DEV)
+    torch.cuda.synchronize()
+    sa, sb = _RawStream(), _RawStream()
+    r1 = gw.nat_6to4(b1, out_arena=out1, stream=sa)
+    gw.reset(stream=sb)
+    r2 = gw.nat_6to4(b2, out_arena=out2, stream=sa)
+    r3 = gw.nat_4to6(b3, out3, oo6, stream=sb)
+    sb.destroy()
+    assert gw.next_port() == pm2.next_port() and gw.size() == pm2.size()
+    torch.cuda.synchronize()
+    for (ob, disp, st), out, want in ((r1, out1, want1), (r2, out2, want2), (r3, out3, want3)):
+        assert (disp.cpu().numpy() == want[2]).all()
+        assert (st.cpu().numpy() == want[3]).all()
+        assert (ob.len.cpu().numpy().view(np.uint16) == want[1]).all()
+        assert (out.cpu().numpy()[: len(want[0])] == want[0][: out.numel()]).all()
+    sa.destroy()
+    gw.close()
