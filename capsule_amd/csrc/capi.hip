@@ -8,6 +8,7 @@
 // RX queue) and no global lock is taken on the launch path.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -84,6 +85,8 @@ struct cgpu_portmap {
   // per-call scratch
   uint32_t *pkt_slot = nullptr;
   uint32_t *chunks = nullptr;
+  cgpu::u32x4 *stash_key = nullptr;
+  uint16_t *stash_port = nullptr;
   uint32_t scratch_n = 0;
   uint32_t calls = 0;  // 6to4 calls: parity of the deferred-list counter
   // recorded on the stream of every call that uses the map: calls on one
@@ -653,6 +656,10 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
   pm->dev.rev_port = (uint32_t *)(p + o_rev_port);
   pm->dev.slots = (cgpu::PortSlot *)(p + o_slots);
   pm->dev.cap_mask = (uint32_t)(cap - 1);
+  // Test hook: CGPU_TEST_NAT64_TAG_MASK=<hex> keeps only those bits of the
+  // claim tags, so distinct keys collide on them and the tail's repair runs.
+  pm->dev.tag_mask = 0xffffffffu;
+  if (const char *tm = getenv("CGPU_TEST_NAT64_TAG_MASK")) pm->dev.tag_mask = (uint32_t)strtoul(tm, nullptr, 16);
   if (hipEventCreateWithFlags(&pm->done, hipEventDisableTiming) != hipSuccess) {
     (void)hipFree(mem);
     delete pm;
@@ -738,10 +745,15 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
     const size_t nb = cgpu::nat64_num_blocks(in->n);
     void *m = nullptr;
     const size_t o_chunks = align_up(4ull * in->n, 256);
-    const size_t o_end = o_chunks + align_up(40ull * nb, 256);  // counts, bases, 8-word masks
+    // counts, bases, 8-word masks per chunk, then the tail's list of tag collisions
+    const size_t o_key = o_chunks + align_up(40ull * nb + 4ull * in->n, 256);
+    const size_t o_port = o_key + align_up(16ull * in->n, 256);
+    const size_t o_end = o_port + align_up(2ull * in->n, 256);
     if (hipMalloc(&m, o_end) != hipSuccess) return fail(CGPU_ENOMEM);
     pm->pkt_slot = (uint32_t *)m;
     pm->chunks = (uint32_t *)((uint8_t *)m + o_chunks);
+    pm->stash_key = (cgpu::u32x4 *)((uint8_t *)m + o_key);
+    pm->stash_port = (uint16_t *)((uint8_t *)m + o_port);
     pm->scratch_n = in->n;
   }
   cgpu::Nat64Args a;
@@ -758,6 +770,8 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   a.status = status;
   a.pkt_slot = pm->pkt_slot;
   a.chunks = pm->chunks;
+  a.stash_key = pm->stash_key;
+  a.stash_port = pm->stash_port;
   a.par = pm->calls & 1u;
   a.room = pm->room;
   a.pm = pm->dev;

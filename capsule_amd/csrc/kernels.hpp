@@ -72,6 +72,8 @@ struct PortMapDev {
                     // deferred[2], tail tickets[2], -, phase-1 chunks done[2];
                     // line 1 (words 32..): the tail's port base and phase-2 flags[2]
   uint32_t cap_mask;
+  uint32_t tag_mask;  // claim-tag bits kept (all; a test build of the map keeps fewer:
+                      // CGPU_TEST_NAT64_TAG_MASK, to exercise the tail's collision repair)
 };
 
 struct Nat64Args {
@@ -87,7 +89,10 @@ struct Nat64Args {
   uint8_t *disposition;
   uint8_t *status;
   uint32_t *pkt_slot;    // scratch [n]: table slot (| kLocalBit: a key new in this batch), or 0xffffffff
-  uint32_t *chunks;      // scratch [10 nblocks]: the tail's chunk counts, bases, first-packet masks
+  uint32_t *chunks;      // scratch [10 nblocks + n]: the tail's chunk counts, bases, first-packet
+                         // masks, then its list of tag collisions
+  u32x4 *stash_key;      // scratch [n]: a tag-joined packet's key (v6 source address) ...
+  uint16_t *stash_port;  // scratch [n]: ... and its TCP source port, verified by the tail
   uint32_t par;          // call parity: selects the per-call counters state[4/6/9/11 + par]
   uint32_t room;         // data room of Mbuf::extend's tailroom model (mbuf.rs:225-233):
                          // 2048 for device batches; 65535 on the mbuf path, whose

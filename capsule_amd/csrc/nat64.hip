@@ -12,31 +12,28 @@
 //
 // The reference assigns gateway ports from a global AtomicU16 (first 1025)
 // in first-seen order of (v6 src, tcp src port).  A batch reproduces that
-// order exactly.  Each direction is one fused kernel in which a quad of 4
-// lanes owns one frame (16 frames per wave, no LDS, no barrier):
-//   - the quad issues its frame's first 256 output bytes as 16-B loads (lane
-//     g: output chunks 4j + g) together with the header chunks, so the frame
-//     streams in while the header is decoded.  A 16-B-aligned frame is read
-//     with aligned loads and realigned by DPP quad permutes (the 20-byte
-//     header-size change is one chunk + one dword); otherwise each lane loads
-//     at the shifted position;
-//   - DPP quad broadcasts give every lane the header dwords; each lane
-//     classifies by the reference control flow (Act / Drop / Abort);
-//   - lane 0 looks the key up in the device port map (6to4: the
-//     open-addressing PORT_MAP; 4to6: the ADDR_MAP arrays, a 16-B address
-//     and a 4-B port per gateway port, read by the whole quad);
-//   - each lane patches its chunks in registers and sums its part of the TCP
-//     span with v_sad_u16; the quad reduces; the lane holding the TCP
-//     checksum field stores it last.
-// A 6to4 frame whose key is not yet committed (first seen in this batch)
-// needs the batch-wide first-seen order, so the fused kernel defers it (its
-// header record goes to global scratch) and a tail kernel finishes it: per
-// 256-packet chunk it counts the first packets of new keys, scans the counts
-// with a decoupled look-back, assigns port = NEXT_PORT + ordinal, commits
-// the keys, and rewrites the chunk's deferred frames.  When no key is new
-// (the steady state) the tail returns at once.  The fused kernel takes the
-// rows path (four whole frames per load and store instruction, see below) when a wave's
-// frames allow it and the quad path otherwise.
+// order exactly.  6to4 is two launches, 4to6 one.
+//
+// The fused kernels (nat64_6to4_fused, nat64_4to6_fused): a wave owns 32
+// frames.  Waves whose frames are 16-B aligned in the input, dword-aligned
+// in the output and short enough for one 256-B row pass take the ROWS path:
+// 16-lane row j loads frame 4r + j in round r (four whole frames per load
+// instruction), bytes 0..95 of each frame reach its own lane through
+// wave-private LDS, the lane classifies the frame by the reference control
+// flow and looks its key up (6to4: the PORT_MAP slot table; 4to6: the
+// ADDR_MAP arrays), the payload is moved by 20 B with DPP row shifts and
+// summed by a DPP row reduction while the lookup is in flight, and row j
+// stores frame 4r + j in one instruction with the header chunks and the TCP
+// checksum patched in.  Other waves take the QUAD path: a quad of lanes per
+// frame (any alignment, any length), DPP quad broadcasts of the header.
+//
+// A 6to4 frame whose key is not yet committed (first seen in this batch) is
+// written with source port 0 and deferred: its key is claimed or joined in
+// the slot table (claim tags, keys published with atomics: probe_port_at),
+// and the tail kernel (nat64_tail) orders the batch's new keys by their
+// first packet, assigns NEXT_PORT + ordinal, commits them, and patches only
+// the deferred frames' port and checksum.  With no new key (the steady
+// state) the tail returns at once.
 #include "capsule_gpu.h"
 #include "device_common.hpp"
 #include "kernels.hpp"
@@ -61,8 +58,13 @@ constexpr uint32_t kFJ = 16u / kFG;          // 16-B chunks per lane per 256-B p
 constexpr uint32_t kNow = 4u;                // record info bit: rewrite in the fused kernel
 constexpr uint32_t kNoSlot = 0xffffffffu;
 constexpr uint32_t kLocalBit = 0x40000000u;  // pkt_slot: key first seen in this batch
-constexpr uint32_t kSlotMask = 0x3fffffffu;
-constexpr uint32_t kReady = 0x40000000u;     // PortSlot ref: the claimer's key words are published
+constexpr uint32_t kClaimBit = 0x20000000u;  // pkt_slot: this packet claimed the slot
+constexpr uint32_t kPatchBit = 0x80000000u;  // pkt_slot (tail repair): a committed key's port
+constexpr uint32_t kSlotMask = 0x1fffffffu;  // slot index (capacity_log2 <= 29)
+#ifndef CGPU_NAT64_TAGJOIN  // 1: joins on the claim tag, verified by the tail; 0: verified in the probe
+#define CGPU_NAT64_TAGJOIN 1
+#endif
+[[maybe_unused]] constexpr uint32_t kReady = 0x40000000u;  // ref (in-kernel verify): key words published
 constexpr uint32_t kV4Addr = 0x017100cbu;    // 203.0.113.1 as LE dword of wire bytes
 // The tailroom model of Mbuf::extend (mbuf.rs:225-233) is Nat64Args::room:
 // RTE_MBUF_DEFAULT_DATAROOM = 2048 for device batches; on the mbuf path the
@@ -294,7 +296,7 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
                                                   const uint32_t (&key)[5], uint32_t h, u32x4 s0,
                                                   u32x4 s1, uint32_t &port) {
   port = 0xffffffffu;
-  const uint32_t tag = key_tag(key);
+  const uint32_t tag = key_tag(key) & a.pm.tag_mask;
   for (uint32_t probe = 0; probe <= a.pm.cap_mask; ++probe) {
     if (probe != 0u) {  // the first slot was loaded by the caller
       const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
@@ -317,14 +319,21 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
     // below the wait).
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (claimed) {
+#if CGPU_NAT64_TAGJOIN
+      // the key words are read behind the kernel boundary only
+      *reinterpret_cast<u32x2 *>(&w[2]) = u32x2{key[0], key[1]};
+      *reinterpret_cast<u32x2 *>(&w[4]) = u32x2{key[2], key[3]};
+      w[6] = key[4];
+#else
 #pragma unroll
       for (int j = 0; j < 5; ++j)
         (void)__hip_atomic_exchange(&w[2 + j], key[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // the exchanges are performed before the flag
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       (void)__hip_atomic_fetch_or(&w[0], kReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
       atomicMin(&w[7], i);
-      return h | kLocalBit;
+      return h | kLocalBit | kClaimBit;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (ref & kPersist) {
@@ -334,7 +343,15 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
         return h;
       }
     } else if (stag == tag) {
-#ifdef CGPU_NAT64_ABL_NOREP  // timing ablation only: tags trusted, no key compare
+#if CGPU_NAT64_TAGJOIN
+      // joined on the tag alone: the key goes to the stash, and the tail
+      // compares it with the slot's key words behind the kernel boundary
+      // (a tag collision is repaired there)
+      a.stash_key[i] = u32x4{key[0], key[1], key[2], key[3]};
+      a.stash_port[i] = (uint16_t)key[4];
+      if (s1[3] > i) atomicMin(&w[7], i);
+      return h | kLocalBit;
+#elif defined(CGPU_NAT64_ABL_NOREP)  // timing ablation only: tags trusted, no key compare
       const bool match = true;
 #else
       for (uint32_t spin = 0; !(ref & kReady) && spin < (1u << 22); ++spin) {
@@ -346,12 +363,14 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
                                  (uint32_t)(k23 >> 32), rd_atomic(&w[6])};
       const bool match = key_eq(key, other);
 #endif
+#if !CGPU_NAT64_TAGJOIN
       if (match) {
         // the key's first packet index (w[7] only decreases, so a value
         // loaded with the slot that is already below i makes the atomic moot)
         if (s1[3] > i) atomicMin(&w[7], i);
         return h | kLocalBit;
       }
+#endif
     }
     h = (h + 1u) & a.pm.cap_mask;
   }
@@ -1098,15 +1117,18 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a
 // The batch's keys first seen in it get NEXT_PORT + (rank of their first
 // packet among the first packets of all new keys): AtomicU16::fetch_add in
 // the reference's packet order (main.rs:45-51).  The fused kernel left each
-// such key's first packet index in its slot (w[7], by atomicMin) and each
-// deferred packet's slot in pkt_slot.  One grid takes 2 * nb tickets in
-// order (nb = chunks of kBlock packets):
-//   ticket c < nb        phase 1, chunk c: which of its packets are a new
-//                        key's first packet (pkt_slot local and w[7] == i): a
-//                        256-bit mask and a count per chunk; the workgroup that
-//                        completes phase 1 last scans the counts into each
-//                        chunk's base ordinal, advances NEXT_PORT and raises
-//                        the phase-2 flag;
+// such key's first packet index in its slot (w[7], by atomicMin), each
+// deferred packet's slot in pkt_slot, and the key of each packet that
+// joined a slot on its claim tag alone in the stash.  One grid takes 2 * nb
+// tickets in order (nb = chunks of kBlock packets):
+//   ticket c < nb        phase 1, chunk c: each tag-joined packet's key is
+//                        compared with its slot's key words (a tag
+//                        collision is listed for the repair below), and the
+//                        packets that are a new key's first packet (w[7] ==
+//                        i) give a 256-bit mask and a count per chunk; the
+//                        workgroup that completes phase 1 last scans the
+//                        counts into each chunk's base ordinal, advances
+//                        NEXT_PORT and raises the phase-2 flag;
 //   ticket nb + c        phase 2, chunk c (after the flag): every deferred
 //                        packet computes its key's port from the first
 //                        packet's chunk base and mask -- no hand-off between
@@ -1115,24 +1137,189 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a
 //                        also commits the key (port, kPersist, ADDR_MAP).
 // Tickets are taken in order by running workgroups and phase 1 never waits,
 // so the phase-2 wait ends (no co-residency needed).  Data handed between
-// workgroups inside the launch (masks, counts, bases, the port base) is
-// stored sc1, drained before the signalling atomic and loaded sc1
-// (MI355X_MICROARCH.md, inter-workgroup visibility: the last arriver told by
-// its add, a flag polled sc1); everything else was written by an earlier
+// workgroups inside the launch (masks, counts, bases, the list of tag
+// collisions, the port base) is stored sc1, drained before the signalling
+// atomic and loaded sc1, on lines no workgroup reads with a plain load in
+// the launch (MI355X_MICROARCH.md, inter-workgroup visibility); the flag is
+// polled with a compare-exchange.  Everything else was written by an earlier
 // launch.  With nothing deferred (the steady state) the grid exits at once.
 // state (128-B line 0): [0] NEXT_PORT [1] entries; by call parity p:
-// [4+p] deferred packets [6+p] tickets [9+p] phase-1 chunks done (the other
-// parity is the previous call's, cleared here for the next one).  The words
-// handed over inside the launch sit on line 1, which nothing reads with a
-// plain load (every workgroup reads line 0 plainly, so its L2 holds it):
-// [32] the port base of the batch in flight, [33+p] the phase-2 flag.
+// [4+p] deferred packets [6+p] tickets [9+p] phase-1 chunks done [14+p]
+// tag collisions (the other parity is the previous call's, cleared here
+// for the next one).  The words handed over inside the launch sit on line
+// 1, which nothing reads with a plain load (every workgroup reads line 0
+// plainly, so its L2 holds it): [32] the port base of the batch in flight,
+// [33+p] the phase-2 flag, [36] repair mode.
 __device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
   return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-constexpr uint32_t kStBase = 32u, kStFlag = 33u;  // state line 1
+constexpr uint32_t kStBase = 32u, kStFlag = 33u, kStMode = 36u;  // state line 1
+constexpr uint32_t kStMism = 14u;                                  // state line 0, by parity
+
+// Whether packet i's stashed key is its slot's key (w = the slot's words).
+__device__ __forceinline__ bool stash_matches(const Nat64Args &a, uint32_t i, const uint32_t *w) {
+  const u32x4 k = a.stash_key[i];
+  return k[0] == w[2] && k[1] == w[3] && k[2] == w[4] && k[3] == w[5] &&
+         (uint32_t)a.stash_port[i] == (w[6] & 0xffffu);
+}
+
+// Phase 1 of chunk c (all kBlock threads): the chunk's first-packet mask
+// words and count, sc1.  Tag-joined packets whose key is not their slot's
+// (collisions) go to the list `mism` (an sc1 entry per packet, counted in
+// state[kStMism + p]); they are never a first packet here.
+__device__ __forceinline__ void chunk_firsts(const Nat64Args &a, uint32_t c, bool verify,
+                                             uint32_t *cnt, uint32_t *cmask, uint32_t *mism,
+                                             uint32_t *s_part) {
+  uint32_t *const st = a.pm.state;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t i = c * kBlock + threadIdx.x;
+  const uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
+  const bool loc = ps != kNoSlot && (ps & kLocalBit);
+  bool bad = false, f = false;
+  if (loc) {
+    const uint32_t *w = a.pm.slots[ps & kSlotMask].w;
+    if (verify && !(ps & kClaimBit)) bad = !stash_matches(a, i, w);
+    f = !bad && w[7] == i;
+  }
+  const uint64_t m = __ballot(f);
+  if (lane == 0) {
+    st_sc1(&cmask[8u * c + 2u * wave], (uint32_t)m);
+    st_sc1(&cmask[8u * c + 2u * wave + 1u], (uint32_t)(m >> 32));
+  }
+  const uint64_t bm = __ballot(bad);
+  if (bm) {  // rare: list the wave's collisions
+    uint32_t at = 0;
+    if (lane == (uint32_t)__builtin_ctzll(bm))
+      at = __hip_atomic_fetch_add(&st[kStMism + a.par], (uint32_t)__popcll(bm), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    at = __shfl(at, (int)__builtin_ctzll(bm));
+    if (bad) st_sc1(&mism[at + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))], i);
+  }
+  const uint32_t n_first = (uint32_t)__syncthreads_count(f);
+  if (threadIdx.x == 0) st_sc1(&cnt[c], n_first);
+  (void)s_part;
+}
+
+// The repair of tag collisions (rare: distinct keys whose claim tags are
+// equal met in a probe chain), by the last phase-1 workgroup: each listed
+// packet looks its key up exactly (its slot's key words were written by the
+// fused kernel; slots this repair claims, by this workgroup) and joins that
+// slot, claims a new one, or takes a committed key's port; the first packet
+// of every slot a colliding packet had joined is recomputed (a collision may
+// have lowered it), and the chunks whose first packets may have changed are
+// counted again.  Phase 2 then reads what the repair may have changed with
+// compare-exchanges (repair mode).
+constexpr uint32_t kRepairSet = 256;  // slots / chunks per pass
+__device__ void tail_repair(const Nat64Args &a, uint32_t nb, uint32_t nmism, const uint32_t *mism,
+                            uint32_t *cnt, uint32_t *cmask, uint32_t *s_part) {
+  __shared__ uint32_t s_slot[kRepairSet], s_min[kRepairSet], s_chunk[4 * kRepairSet];
+  __shared__ uint32_t s_ns, s_nc, s_all;
+  if (threadIdx.x == 0) {
+    s_ns = 0u;
+    s_nc = 0u;
+    s_all = 0u;
+  }
+  __syncthreads();
+  // 1. the listed packets, one by one (thread 0): exact lookups
+  if (threadIdx.x == 0) {
+    auto add_chunk = [&](uint32_t pkt) {
+      const uint32_t ch = pkt / kBlock;
+      for (uint32_t q = 0; q < s_nc; ++q)
+        if (s_chunk[q] == ch) return;
+      if (s_nc < 4u * kRepairSet) s_chunk[s_nc++] = ch;
+      else s_all = 1u;
+    };
+    for (uint32_t q = 0; q < nmism; ++q) {
+      const uint32_t m = ld_sc1(&mism[q]);
+      const uint32_t wrong = a.pkt_slot[m] & kSlotMask;
+      uint32_t k = 0;
+      for (; k < s_ns; ++k)
+        if (s_slot[k] == wrong) break;
+      if (k == s_ns) {
+        if (s_ns < kRepairSet) {
+          s_slot[s_ns] = wrong;
+          s_min[s_ns] = 0xffffffffu;
+          ++s_ns;
+        } else {
+          s_all = 1u;  // more wrong slots than a pass holds: recount every chunk
+        }
+      }
+      add_chunk(m);
+      add_chunk(a.pm.slots[wrong].w[7]);  // the wrong slot's first packet so far
+      const u32x4 sk = a.stash_key[m];
+      const uint32_t key[5] = {sk[0], sk[1], sk[2], sk[3], (uint32_t)a.stash_port[m]};
+      uint32_t h = key_hash(key) & a.pm.cap_mask, res = kNoSlot;
+      for (uint32_t probe = 0; probe <= a.pm.cap_mask; ++probe, h = (h + 1u) & a.pm.cap_mask) {
+        uint32_t *w = a.pm.slots[h].w;
+        const uint32_t other[5] = {w[2], w[3], w[4], w[5], w[6] & 0xffffu};
+        if (w[0] == 0u) {  // a new key after all: claim it
+          w[1] = key_tag(key) & a.pm.tag_mask;
+          w[2] = key[0];
+          w[3] = key[1];
+          w[4] = key[2];
+          w[5] = key[3];
+          w[6] = key[4];
+          w[7] = m;
+          w[0] = m + 1u;
+          res = h | kLocalBit | kClaimBit;
+          break;
+        }
+        if (!key_eq(key, other)) continue;
+        if (w[0] & kPersist) {  // a committed key: its port (the frame is patched with it)
+          res = h | kPatchBit;
+        } else {
+          add_chunk(w[7]);
+          if (m < w[7]) w[7] = m;
+          res = h | kLocalBit;
+        }
+        break;
+      }
+      if (res == kNoSlot) {  // no room: the packet aborts (TABLE_FULL)
+        a.disposition[m] = CGPU_ABORT;
+        a.status[m] = CGPU_PKT_TABLE_FULL;
+        a.out_len[m] = 0;
+      }
+      a.pkt_slot[m] = res;
+    }
+  }
+  __syncthreads();
+  // 2. the first packet of each slot a collision had joined: the minimum
+  // over the packets that belong to it now (passes of kRepairSet slots)
+  const uint32_t ns = s_ns;
+  for (uint32_t i = threadIdx.x; i < a.n; i += kBlock) {
+    const uint32_t ps = a.pkt_slot[i];
+    if (ps == kNoSlot || !(ps & kLocalBit)) continue;
+    const uint32_t sl = ps & kSlotMask;
+    for (uint32_t k = 0; k < ns; ++k)
+      if (s_slot[k] == sl) atomicMin(&s_min[k], i);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (uint32_t k = 0; k < ns; ++k) {
+      a.pm.slots[s_slot[k]].w[7] = s_min[k];
+      const uint32_t ch = s_min[k] / kBlock;
+      bool have = false;
+      for (uint32_t q = 0; q < s_nc; ++q) have |= s_chunk[q] == ch;
+      if (!have) {
+        if (s_nc < 4u * kRepairSet) s_chunk[s_nc++] = ch;
+        else s_all = 1u;
+      }
+    }
+  __syncthreads();
+  // (a second pass for more than kRepairSet wrong slots)
+  // 3. count the affected chunks again (every chunk when the sets overflowed)
+  const uint32_t nc = s_all ? nb : s_nc;
+  for (uint32_t q = 0; q < nc; ++q) {
+    const uint32_t c = s_all ? q : s_chunk[q];
+    chunk_firsts(a, c, false, cnt, cmask, nullptr, s_part);
+  }
+  if (threadIdx.x == 0) st_sc1(&a.pm.state[kStMode], 1u);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+}
 
 // The last phase-1 workgroup: exclusive scan of the chunk counts into the
 // chunk bases, the port base, NEXT_PORT advanced (AtomicU16 wrap), the flag.
@@ -1172,6 +1359,8 @@ __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const
   if (threadIdx.x == 0) st_sc1(&st[kStFlag + a.par], 1u);
 }
 
+__device__ __forceinline__ uint32_t rd_cas(uint32_t *p) { return atomicCAS(p, 0u, 0u); }
+
 __global__ __launch_bounds__(kBlock) void nat64_tail(Nat64Args a, uint32_t nb) {
   __shared__ uint32_t s_ticket, s_last;
   __shared__ uint32_t s_part[kBlock + 1];
@@ -1181,75 +1370,88 @@ __global__ __launch_bounds__(kBlock) void nat64_tail(Nat64Args a, uint32_t nb) {
     st[4u + (p ^ 1u)] = 0u;
     st[6u + (p ^ 1u)] = 0u;
     st[9u + (p ^ 1u)] = 0u;
+    st[kStMism + (p ^ 1u)] = 0u;
     st[kStFlag + (p ^ 1u)] = 0u;
   }
   if (st[4u + p] == 0u) return;  // nothing deferred: no new key
   uint32_t *const cnt = a.chunks, *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t *const mism = a.chunks + 10u * nb;  // the tag collisions (packet indices)
   for (;;) {
     if (threadIdx.x == 0) s_ticket = atomicAdd(&st[6u + p], 1u);
     __syncthreads();
     const uint32_t t = s_ticket;
     if (t >= 2u * nb) return;  // workgroup-uniform
     if (t < nb) {
-      // phase 1: chunk t's first packets of new keys
-      const uint32_t i = t * kBlock + threadIdx.x;
-      const uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
-      const bool f = ps != kNoSlot && (ps & kLocalBit) && a.pm.slots[ps & kSlotMask].w[7] == i;
-      const uint64_t m = __ballot(f);
-      if (lane == 0) {
-        st_sc1(&cmask[8u * t + 2u * wave], (uint32_t)m);
-        st_sc1(&cmask[8u * t + 2u * wave + 1u], (uint32_t)(m >> 32));
-      }
-      const uint32_t c = (uint32_t)__syncthreads_count(f);
-      if (threadIdx.x == 0) st_sc1(&cnt[t], c);
+      chunk_firsts(a, t, CGPU_NAT64_TAGJOIN != 0, cnt, cmask, mism, s_part);
       __builtin_amdgcn_s_waitcnt(0);  // every storing wave drains before the arrival
       __syncthreads();
       if (threadIdx.x == 0)
         s_last = __hip_atomic_fetch_add(&st[9u + p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1u;
       __syncthreads();
-      if (s_last) tail_scan(a, nb, cnt, cbase, s_part);
+      if (s_last) {  // the workgroup that completed phase 1 last
+        __shared__ uint32_t s_nm;
+        if (threadIdx.x == 0) {
+          s_nm = rd_cas(&st[kStMism + p]);
+          st_sc1(&st[kStMode], 0u);
+        }
+        __syncthreads();
+        if (s_nm) tail_repair(a, nb, s_nm, mism, cnt, cmask, s_part);
+        tail_scan(a, nb, cnt, cbase, s_part);
+      }
       __syncthreads();  // s_ticket, s_last, s_part are rewritten next round
       continue;
     }
     // phase 2: chunk t - nb, once every chunk base is known (the flag is
     // polled with a compare-exchange, performed at the coherence point)
+    __shared__ uint32_t s_base, s_mode;
     if (threadIdx.x == 0) {
-      while (atomicCAS(&st[kStFlag + p], 0u, 0u) == 0u) __builtin_amdgcn_s_sleep(2);
-      s_last = ld_sc1(&st[kStBase]);
+      // (bounded, ~2 s: a wait that never ended would mean a broken
+      // protocol; the results are then wrong, but the GPU is not hung)
+      for (uint32_t spin = 0; rd_cas(&st[kStFlag + p]) == 0u && spin < (1u << 24); ++spin)
+        __builtin_amdgcn_s_sleep(2);
+      s_base = ld_sc1(&st[kStBase]);
+      s_mode = ld_sc1(&st[kStMode]);
     }
     __syncthreads();
-    const uint32_t port_base = s_last;
+    const uint32_t port_base = s_base;
+    const bool repaired = s_mode != 0u;  // the repair may have changed pkt_slot and slot words
     const uint32_t i = (t - nb) * kBlock + threadIdx.x;
-    const uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
-    if (ps != kNoSlot && (ps & kLocalBit)) {
+    uint32_t ps = kNoSlot;
+    if (i < a.n) ps = repaired ? rd_cas(&a.pkt_slot[i]) : a.pkt_slot[i];
+    if (ps != kNoSlot && (ps & (kLocalBit | kPatchBit))) {
       uint32_t *w = a.pm.slots[ps & kSlotMask].w;
-      const uint32_t fi = w[7];  // the key's first packet
-      const uint32_t fc = fi / kBlock, fb = fi % kBlock;
-      uint32_t below = 0;
+      uint32_t port;
+      if (ps & kLocalBit) {
+        const uint32_t fi = repaired ? rd_cas(&w[7]) : w[7];  // the key's first packet
+        const uint32_t fc = fi / kBlock, fb = fi % kBlock;
+        uint32_t below = 0;
 #pragma unroll
-      for (uint32_t j = 0; j < 8u; ++j) {
-        const uint32_t mw = ld_sc1(&cmask[8u * fc + j]);
-        const uint32_t lo = 32u * j;
-        below += (uint32_t)__builtin_popcount(fb >= lo + 32u ? mw : (fb > lo ? mw & ((1u << (fb - lo)) - 1u) : 0u));
-      }
-      const uint32_t ordinal = ld_sc1(&cbase[fc]) + below;
-      const uint32_t port = (port_base + ordinal) & 0xffffu;  // NEXT_PORT.fetch_add order
-      if (fi == i) {
-        const u32x4 k0 = *reinterpret_cast<const u32x4 *>(w);      // ref, tag, key[0..1]
-        const u32x4 k1 = *reinterpret_cast<const u32x4 *>(w + 4);  // key[2..4]
-        // ADDR_MAP.insert_new(port, key) (main.rs:50): the first mapping of a
-        // port wins, also after NEXT_PORT wraps.  This call's ordinals o and
-        // o + 65536k share a port, so only its first lap (o < 65536) can be
-        // first, and only if no earlier call mapped the port: one writer per
-        // entry, no race.
-        if (ordinal < 65536u && !(a.pm.rev_port[port] & kRevValid)) {
-          a.pm.rev_addr[port] = u32x4{k0[2], k0[3], k1[0], k1[1]};
-          a.pm.rev_port[port] = (k1[2] & 0xffffu) | kRevValid;
+        for (uint32_t j = 0; j < 8u; ++j) {
+          const uint32_t mw = ld_sc1(&cmask[8u * fc + j]);
+          const uint32_t lo = 32u * j;
+          below += (uint32_t)__builtin_popcount(fb >= lo + 32u ? mw : (fb > lo ? mw & ((1u << (fb - lo)) - 1u) : 0u));
         }
-        // PORT_MAP.insert_new (main.rs:49): the key, committed for later batches
-        w[6] = (k1[2] & 0xffffu) | (port << 16);
-        w[0] = kPersist;
+        const uint32_t ordinal = ld_sc1(&cbase[fc]) + below;
+        port = (port_base + ordinal) & 0xffffu;  // NEXT_PORT.fetch_add order
+        if (fi == i) {
+          uint32_t kw[5];
+#pragma unroll
+          for (int j = 0; j < 5; ++j) kw[j] = repaired ? rd_cas(&w[2 + j]) : w[2 + j];
+          // ADDR_MAP.insert_new(port, key) (main.rs:50): the first mapping of
+          // a port wins, also after NEXT_PORT wraps.  This call's ordinals o
+          // and o + 65536k share a port, so only its first lap (o < 65536)
+          // can be first, and only if no earlier call mapped the port: one
+          // writer per entry, no race.
+          if (ordinal < 65536u && !(a.pm.rev_port[port] & kRevValid)) {
+            a.pm.rev_addr[port] = u32x4{kw[0], kw[1], kw[2], kw[3]};
+            a.pm.rev_port[port] = (kw[4] & 0xffffu) | kRevValid;
+          }
+          // PORT_MAP.insert_new (main.rs:49): the key, committed for later batches
+          w[6] = (kw[4] & 0xffffu) | (port << 16);
+          w[0] = kPersist;
+        }
+      } else {  // (repair) a committed key found for a colliding packet
+        port = rd_cas(&w[6]) >> 16;
       }
       // The frame was written with source port 0 and the checksum c0 of
       // that frame; set the port and patch the checksum, ~fold(~c0 + port)
@@ -1267,7 +1469,7 @@ __global__ __launch_bounds__(kBlock) void nat64_tail(Nat64Args a, uint32_t nb) {
       tcp[16] = (uint8_t)(c >> 8);
       tcp[17] = (uint8_t)c;
     }
-    __syncthreads();  // s_ticket is rewritten next round
+    __syncthreads();  // s_ticket, s_base, s_mode are rewritten next round
   }
 }
 

@@ -11,9 +11,9 @@ step launch_gap 120 tools/launch_gap
 step recon_tests 600 python -u -m pytest tests/test_reconcile_gpu.py -x -q --timeout 120 --timeout-method thread
 step nat64_tests 900 python -u -m pytest tests/test_nat64_gpu.py tests/test_bench_parity_gpu.py tests/test_nat64_mbufs_gpu.py -x -v --timeout 300 --timeout-method thread
 export CFG=nat64_cold
-step cold_stats 600 bash scripts/ab_stats.sh base norep new
+step cold_stats 600 bash scripts/ab_stats.sh base norep new new_verify
 export CFG=nat64
-step steady_stats 600 bash scripts/ab_stats.sh base new
+step steady_stats 600 bash scripts/ab_stats.sh base new new_verify
 export AB_STEPS=300
 step recon_ab 600 bash scripts/ab_variants.sh "reconcile64 reconcile_imix" "FETCH_SIZE;WRITE_SIZE" recon_fields recon_whole
 step cold_pmc 900 bash scripts/ab_variants.sh nat64_cold "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD;FETCH_SIZE" base norep new

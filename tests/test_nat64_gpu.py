@@ -425,3 +425,31 @@ def test_portmap_calls_ordered_across_streams(ctx):
         assert (out.cpu().numpy()[: len(want[0])] == want[0][: out.numel()]).all()
     sa.destroy()
     gw.close()
+
+
+@pytest.mark.parametrize("mask", ["0", "1"])
+def test_claim_tag_collisions_repaired(ctx, monkeypatch, mask):
+    """The fused kernel joins a batch-local slot on its 32-bit claim tag; the
+    tail compares every joined packet's key with the slot's and repairs a
+    collision (distinct keys, equal tags).  With the tags cut to 0 or 1 bit
+    (CGPU_TEST_NAT64_TAG_MASK, read when the map is created) every meeting
+    of two keys in a probe chain is a collision: ports, frames, map state and
+    the 4to6 replies must still equal the oracle's, cold and steady."""
+    from capsule_amd import packets
+
+    monkeypatch.setenv("CGPU_TEST_NAT64_TAG_MASK", mask)
+    gw = packets.Nat64Gateway(ctx, capacity_log2=10)  # 1024 slots, load 0.3
+    monkeypatch.delenv("CGPU_TEST_NAT64_TAG_MASK")
+    pm = oracle_lib.PortMap()
+    a, o, l = synth.nat64_stream(6000, n_keys=300, seed=81, drop_frac=0.05)
+    half = int(o[3000])
+    parts = [(a[:half], o[:3000], l[:3000]), (a[half:], o[3000:] - np.uint32(half), l[3000:]),
+             (a, o, l)]
+    for aa, oo, ll in parts:  # first sight of most keys, then the rest, then all committed
+        out, olen, disp, _ = _nat_both(ctx, gw, pm, "6to4", aa, oo, ll, oo, len(aa) + 64)
+    assert gw.size() == pm.size() and gw.next_port() == pm.next_port()
+    keep = np.nonzero(disp == N.ACT)[0]
+    ra, ro, rl = synth.nat64_replies(out, o[keep], olen[keep])
+    o6 = (np.arange(len(ro), dtype=np.int64) * 256).astype(np.uint32)
+    _nat_both(ctx, gw, pm, "4to6", ra, ro, rl, o6, 256 * len(ro) + 64)
+    gw.close()
