@@ -16,6 +16,13 @@
 #include "capsule_gpu.h"
 #include "kernels.hpp"
 
+#ifndef CGPU_NAT64_EXT_EVENT  // 1: a nat64 call's completion event is its last kernel's stop event
+#define CGPU_NAT64_EXT_EVENT 1
+#endif
+#ifndef CGPU_NAT64_ALWAYS_WAIT  // 1: every nat64 call waits for the map's previous call
+#define CGPU_NAT64_ALWAYS_WAIT 1
+#endif
+
 namespace {
 
 thread_local int g_last_error = 0;
@@ -775,15 +782,30 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   a.par = pm->calls & 1u;
   a.room = pm->room;
   a.pm = pm->dev;
-  if (stream != pm->last_stream &&
-      hipStreamWaitEvent((hipStream_t)stream, pm->done, 0) != hipSuccess)
+  // Calls on one map are ordered: behind the previous call's completion
+  // event, whatever stream it ran on (a wait on the same stream is already
+  // satisfied; comparing stream handles instead would trust a handle the
+  // caller may have destroyed and had handed out again).
+#if CGPU_NAT64_ALWAYS_WAIT
+  if (hipStreamWaitEvent((hipStream_t)stream, pm->done, 0) != hipSuccess) return fail(CGPU_EIO);
+#else
+  if (stream != pm->last_stream && hipStreamWaitEvent((hipStream_t)stream, pm->done, 0) != hipSuccess)
     return fail(CGPU_EIO);
   pm->last_stream = stream;
-  hipError_t e = to4 ? cgpu::launch_nat64_6to4(a, (hipStream_t)stream)
-                     : cgpu::launch_nat64_4to6(a, (hipStream_t)stream);
+#endif
+#if CGPU_NAT64_EXT_EVENT
+  // the completion event rides on the call's last kernel (no marker packet)
+  hipError_t e = to4 ? cgpu::launch_nat64_6to4(a, (hipStream_t)stream, pm->done)
+                     : cgpu::launch_nat64_4to6(a, (hipStream_t)stream, pm->done);
+  if (e != hipSuccess) return hip_fail(e);
+  if (to4) ++pm->calls;
+#else
+  hipError_t e = to4 ? cgpu::launch_nat64_6to4(a, (hipStream_t)stream, nullptr)
+                     : cgpu::launch_nat64_4to6(a, (hipStream_t)stream, nullptr);
   if (e != hipSuccess) return hip_fail(e);
   if (to4) ++pm->calls;
   if (hipEventRecord(pm->done, (hipStream_t)stream) != hipSuccess) return fail(CGPU_EIO);
+#endif
   return ok();
 }
 

@@ -100,8 +100,8 @@ struct Nat64Args {
   PortMapDev pm;
 };
 
-hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s);
-hipError_t launch_nat64_4to6(const Nat64Args &a, hipStream_t s);
+hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s, hipEvent_t done);
+hipError_t launch_nat64_4to6(const Nat64Args &a, hipStream_t s, hipEvent_t done);
 hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStream_t s);
 uint32_t nat64_num_blocks(uint32_t n);
 

@@ -34,6 +34,8 @@
 // first packet, assigns NEXT_PORT + ordinal, commits them, and patches only
 // the deferred frames' port and checksum.  With no new key (the steady
 // state) the tail returns at once.
+#include <hip/hip_ext.h>
+
 #include "capsule_gpu.h"
 #include "device_common.hpp"
 #include "kernels.hpp"
@@ -1833,7 +1835,10 @@ hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStr
   return hipGetLastError();
 }
 
-hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s) {
+// done (may be null): recorded when the call's last kernel completes, as
+// the kernel's own completion (hipExtLaunchKernelGGL's stop event) rather
+// than a separate marker packet behind it
+hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s, hipEvent_t done) {
   if (a.n == 0) return hipSuccess;
   const uint32_t nb = nat64_num_blocks(a.n);
   const uint32_t fpb = (kBlock / 64u) * kRowFrames;  // fused: kRowFrames frames per wave
@@ -1842,14 +1847,14 @@ hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s) {
   // the tail (order + the deferred frames' ports) takes 2 nb tickets; in the
   // steady state (no new key) it returns at once
   const uint32_t tg = 2u * nb < kTailGrid ? 2u * nb : kTailGrid;
-  hipLaunchKernelGGL(nat64_tail, dim3(tg), dim3(kBlock), 0, s, a, nb);
+  hipExtLaunchKernelGGL(nat64_tail, dim3(tg), dim3(kBlock), 0, s, nullptr, done, 0, a, nb);
   return hipGetLastError();
 }
 
-hipError_t launch_nat64_4to6(const Nat64Args &a, hipStream_t s) {
+hipError_t launch_nat64_4to6(const Nat64Args &a, hipStream_t s, hipEvent_t done) {
   if (a.n == 0) return hipSuccess;
   const uint32_t fpb = (kBlock / 64u) * kRowFrames;  // kRowFrames frames per wave
-  hipLaunchKernelGGL(nat64_4to6_fused, dim3((a.n + fpb - 1) / fpb), dim3(kBlock), 0, s, a);
+  hipExtLaunchKernelGGL(nat64_4to6_fused, dim3((a.n + fpb - 1) / fpb), dim3(kBlock), 0, s, nullptr, done, 0, a);
   return hipGetLastError();
 }
 

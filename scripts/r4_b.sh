@@ -17,3 +17,4 @@ step steady_stats 600 bash scripts/ab_stats.sh base new new_verify
 export AB_STEPS=300
 step recon_ab 600 bash scripts/ab_variants.sh "reconcile64 reconcile_imix" "FETCH_SIZE;WRITE_SIZE" recon_fields recon_whole
 step cold_pmc 900 bash scripts/ab_variants.sh nat64_cold "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD;FETCH_SIZE" base norep new
+step gap_ab 900 bash scripts/ab_variants.sh "nat64 nat64_4to6" "-" base new new_rec new_nowait
