@@ -645,8 +645,8 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
   DeviceGuard dg(ctx->device);
   if (!dg.ok()) return fail(CGPU_ENODEV);
   const size_t cap = (size_t)1 << capacity_log2;
-  const size_t o_rev_addr = 256, o_rev_port = o_rev_addr + 65536 * 16;
-  const size_t o_slots = o_rev_port + 65536 * 4;
+  const size_t o_rev = 256;
+  const size_t o_slots = o_rev + 65536 * 20;
   const size_t bytes = o_slots + cap * sizeof(cgpu::PortSlot);
   void *mem = nullptr;
   if (hipMalloc(&mem, bytes) != hipSuccess) return fail(CGPU_ENOMEM);
@@ -659,8 +659,7 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
   pm->mem = mem;
   uint8_t *p = (uint8_t *)mem;
   pm->dev.state = (uint32_t *)p;
-  pm->dev.rev_addr = (cgpu::u32x4 *)(p + o_rev_addr);
-  pm->dev.rev_port = (uint32_t *)(p + o_rev_port);
+  pm->dev.rev = (uint32_t *)(p + o_rev);
   pm->dev.slots = (cgpu::PortSlot *)(p + o_slots);
   pm->dev.cap_mask = (uint32_t)(cap - 1);
   // Test hook: CGPU_TEST_NAT64_TAG_MASK=<hex> keeps only those bits of the

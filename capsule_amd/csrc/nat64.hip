@@ -1444,9 +1444,11 @@ __global__ __launch_bounds__(kBlock) void nat64_tail(Nat64Args a, uint32_t nb) {
           // and o + 65536k share a port, so only its first lap (o < 65536)
           // can be first, and only if no earlier call mapped the port: one
           // writer per entry, no race.
-          if (ordinal < 65536u && !(a.pm.rev_port[port] & kRevValid)) {
-            a.pm.rev_addr[port] = u32x4{kw[0], kw[1], kw[2], kw[3]};
-            a.pm.rev_port[port] = (kw[4] & 0xffffu) | kRevValid;
+          uint32_t *e = a.pm.rev + 5u * port;
+          if (ordinal < 65536u && !(e[4] & kRevValid)) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) e[j] = kw[j];
+            e[4] = (kw[4] & 0xffffu) | kRevValid;
           }
           // PORT_MAP.insert_new (main.rs:49): the key, committed for later batches
           w[6] = (kw[4] & 0xffffu) | (port << 16);
@@ -1476,8 +1478,8 @@ __global__ __launch_bounds__(kBlock) void nat64_tail(Nat64Args a, uint32_t nb) {
 }
 
 // ============================ 4to6 direction =================================
-// Classify, look the TCP destination port up in ADDR_MAP (rev_addr[port],
-// rev_port[port] = the v6 key itself, two independent reads), build the
+// Classify, look the TCP destination port up in ADDR_MAP (rev[port]: the v6
+// key itself, one 20-B entry), build the
 // IPv6 header, then the quad
 // rewrite with the input shifted by -20 bytes behind the 40-byte header (the
 // TCP checksum field, output bytes 70+4k, is in chunk 4).
@@ -1521,6 +1523,15 @@ __device__ __forceinline__ void classify4(const uint32_t (&P)[20], uint32_t len,
       }
     }
   }
+}
+
+// ADDR_MAP[port]: the v6 address and the port word (| kRevValid), one 20-B
+// entry read as a dwordx4 and a dword (buffer loads: any dword alignment)
+__device__ __forceinline__ void rev_read(const PortMapDev &pm, uint32_t port, u32x4 &addr,
+                                         uint32_t &rport) {
+  const rsrc_t rr = make_rsrc(pm.rev, 65536u * 20u);
+  addr = __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(20u * port), 0, 0);
+  rport = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)(20u * port + 16u), 0, 0);
 }
 
 // The IPv6 header of a 4to6 frame (Ipv6Header::default + set_dscp / ecn /
@@ -1699,8 +1710,7 @@ __device__ __forceinline__ bool rows_4to6(const Nat64Args &a, rsrc_t rs, rsrc_t 
   u32x4 s0 = {0u, 0u, 0u, 0u};
   uint32_t rport = 0u;
   if (act0) {
-    s0 = a.pm.rev_addr[v.gw_port];
-    rport = a.pm.rev_port[v.gw_port];
+    rev_read(a.pm, v.gw_port, s0, rport);
   }
   const uint32_t nl = len + 20u;  // meaningful for ACT frames
   if (mine) {
@@ -1762,8 +1772,7 @@ __device__ __forceinline__ void quad_4to6(const Nat64Args &a, rsrc_t rs, rsrc_t 
   u32x4 s0 = {0u, 0u, 0u, 0u};
   uint32_t rport = 0u;
   if (d.valid && v.disp == CGPU_ACT) {
-    s0 = a.pm.rev_addr[v.gw_port];
-    rport = a.pm.rev_port[v.gw_port];
+    rev_read(a.pm, v.gw_port, s0, rport);
     addr_map_check(a, d.len, rport, v);
   }
   const bool act = d.valid && v.disp == CGPU_ACT;
@@ -1808,8 +1817,8 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
     s[1] = u32x4{0u, 0u, 0u, 0xffffffffu};
   }
   if (i < 65536u) {
-    pm.rev_addr[i] = u32x4{0u, 0u, 0u, 0u};
-    pm.rev_port[i] = 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 5u; ++j) pm.rev[5u * i + j] = 0u;
   }
   if (i == 0) {
     pm.state[0] = first_port;  // NEXT_PORT
