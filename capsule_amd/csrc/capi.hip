@@ -748,11 +748,11 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
     if (pm->pkt_slot) (void)hipFree(pm->pkt_slot);
     pm->pkt_slot = nullptr;
     pm->scratch_n = 0;
-    const size_t nb = cgpu::nat64_num_blocks(in->n);
     void *m = nullptr;
     const size_t o_chunks = align_up(4ull * in->n, 256);
-    // counts, bases, 8-word masks per chunk, then the tail's list of tag collisions
-    const size_t o_key = o_chunks + align_up(40ull * nb + 4ull * in->n, 256);
+    // counts, bases, 8-word masks per chunk, the tail's list of tag
+    // collisions and its control lines
+    const size_t o_key = o_chunks + align_up(cgpu::nat64_chunk_bytes(in->n), 256);
     const size_t o_port = o_key + align_up(16ull * in->n, 256);
     const size_t o_end = o_port + align_up(2ull * in->n, 256);
     if (hipMalloc(&m, o_end) != hipSuccess) return fail(CGPU_ENOMEM);
@@ -760,6 +760,14 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
     pm->chunks = (uint32_t *)((uint8_t *)m + o_chunks);
     pm->stash_key = (cgpu::u32x4 *)((uint8_t *)m + o_key);
     pm->stash_port = (uint16_t *)((uint8_t *)m + o_port);
+    // the tail's control lines start at zero; its last workgroup leaves them so
+    if (hipMemsetAsync((uint8_t *)pm->chunks + cgpu::nat64_ctl_offset(in->n), 0,
+                       cgpu::nat64_chunk_bytes(in->n) - cgpu::nat64_ctl_offset(in->n),
+                       (hipStream_t)stream) != hipSuccess) {
+      (void)hipFree(m);
+      pm->pkt_slot = nullptr;
+      return fail(CGPU_EIO);
+    }
     pm->scratch_n = in->n;
   }
   cgpu::Nat64Args a;
@@ -776,6 +784,7 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   a.status = status;
   a.pkt_slot = pm->pkt_slot;
   a.chunks = pm->chunks;
+  a.ctl = pm->chunks + cgpu::nat64_ctl_offset(pm->scratch_n) / 4u;
   a.stash_key = pm->stash_key;
   a.stash_port = pm->stash_port;
   a.par = pm->calls & 1u;

@@ -70,9 +70,7 @@ struct PortMapDev {
   PortSlot *slots;  // [cap]
   uint32_t *rev;      // [65536 * 5] ADDR_MAP: per gateway port, the address (4 dwords)
                       // and the port | kRevValid, 20 B per port, packed
-  uint32_t *state;  // [64]: line 0: next_port, entries, -, -, then per call parity:
-                    // deferred[2], tail tickets[2], -, phase-1 chunks done[2];
-                    // line 1 (words 32..): the tail's port base and phase-2 flags[2]
+  uint32_t *state;  // [64]: next_port, entries, -, -, then per call parity: deferred[2]
   uint32_t cap_mask;
   uint32_t tag_mask;  // claim-tag bits kept (all; a test build of the map keeps fewer:
                       // CGPU_TEST_NAT64_TAG_MASK, to exercise the tail's collision repair)
@@ -91,11 +89,14 @@ struct Nat64Args {
   uint8_t *disposition;
   uint8_t *status;
   uint32_t *pkt_slot;    // scratch [n]: table slot (| kLocalBit: a key new in this batch), or 0xffffffff
-  uint32_t *chunks;      // scratch [10 nblocks + n]: the tail's chunk counts, bases, first-packet
-                         // masks, then its list of tag collisions
+  uint32_t *chunks;      // scratch [10 nblocks + n (rounded up to 32) + 33 * 32]: the tail's
+                         // chunk counts, bases, first-packet masks, its list of tag
+                         // collisions, then its control lines (zero between calls)
+  uint32_t *ctl;         // scratch: the tail's control lines (at a place fixed for the
+                         // scratch's capacity, not the call's n: zeroed once)
   u32x4 *stash_key;      // scratch [n]: a tag-joined packet's key (v6 source address) ...
   uint16_t *stash_port;  // scratch [n]: ... and its TCP source port, verified by the tail
-  uint32_t par;          // call parity: selects the per-call counters state[4/6/9/11 + par]
+  uint32_t par;          // call parity: selects the deferred flag state[4 + par]
   uint32_t room;         // data room of Mbuf::extend's tailroom model (mbuf.rs:225-233):
                          // 2048 for device batches; 65535 on the mbuf path, whose
                          // scatter checks each mbuf's real tailroom instead
@@ -106,6 +107,10 @@ hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s, hipEvent_t done)
 hipError_t launch_nat64_4to6(const Nat64Args &a, hipStream_t s, hipEvent_t done);
 hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStream_t s);
 uint32_t nat64_num_blocks(uint32_t n);
+// bytes of Nat64Args::chunks for up to n packets, and the offset of the
+// control lines in it (Nat64Args::ctl, zeroed once when allocated)
+size_t nat64_chunk_bytes(uint32_t n);
+size_t nat64_ctl_offset(uint32_t n);
 
 // ---- zero-copy rte_mbuf ingress (ingress.hip) ------------------------------
 struct HostRegion {

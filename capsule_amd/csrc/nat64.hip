@@ -767,12 +767,18 @@ __device__ __forceinline__ void rewrite_quad(const Nat64Args &a, rsrc_t rs, rsrc
 
 // Count the wave's deferred frames (flag set in their lane), one atomic per
 // wave: the tail kernel returns at once when the count is 0.
+// Flag that the batch has deferred frames (the tail returns at once
+// without).  A plain store of 1 by one lane of each such wave: an atomic add
+// on one word from every wave of a cold batch (32 k waves) serialized at
+// that word's memory-side atomic unit, about 90 adds per us, and took the
+// fused kernel from 110 to 400 us; plain stores of the same value merge in
+// the XCDs' L2s and reach memory at the kernel boundary.
 __device__ __forceinline__ void defer_append(const Nat64Args &a, uint32_t lane, bool flag,
                                              uint32_t i) {
   (void)i;
   const uint64_t dm = __ballot(flag);
   if (!dm) return;
-  if (lane == (uint32_t)__builtin_ctzll(dm)) atomicAdd(&a.pm.state[4u + a.par], (uint32_t)__popcll(dm));
+  if (lane == (uint32_t)__builtin_ctzll(dm)) a.pm.state[4u + a.par] = 1u;
 }
 
 // The general path: one quad per frame (any alignment, any length); `i` is
@@ -1115,51 +1121,60 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a
   for (uint32_t q = 0; q < kRowFrames / 16u; ++q) quad_6to4(a, rs, ors, base + 16u * q + lane / 4u, lane);
 }
 
-// ---- the tail kernel: order the batch's new keys, finish their frames ------
+// ---- the tail: order the batch's new keys, finish their frames --------------
 // The batch's keys first seen in it get NEXT_PORT + (rank of their first
 // packet among the first packets of all new keys): AtomicU16::fetch_add in
 // the reference's packet order (main.rs:45-51).  The fused kernel left each
 // such key's first packet index in its slot (w[7], by atomicMin), each
 // deferred packet's slot in pkt_slot, and the key of each packet that
-// joined a slot on its claim tag alone in the stash.  One grid takes 2 * nb
-// tickets in order (nb = chunks of kBlock packets):
-//   ticket c < nb        phase 1, chunk c: each tag-joined packet's key is
-//                        compared with its slot's key words (a tag
-//                        collision is listed for the repair below), and the
-//                        packets that are a new key's first packet (w[7] ==
-//                        i) give a 256-bit mask and a count per chunk; the
-//                        workgroup that completes phase 1 last scans the
-//                        counts into each chunk's base ordinal, advances
-//                        NEXT_PORT and raises the phase-2 flag;
-//   ticket nb + c        phase 2, chunk c (after the flag): every deferred
-//                        packet computes its key's port from the first
-//                        packet's chunk base and mask -- no hand-off between
-//                        packets of one key -- and patches its frame (the fused
-//                        kernel wrote it with source port 0); a first packet
-//                        also commits the key (port, kPersist, ADDR_MAP).
-// Tickets are taken in order by running workgroups and phase 1 never waits,
-// so the phase-2 wait ends (no co-residency needed).  Data handed between
-// workgroups inside the launch (masks, counts, bases, the list of tag
-// collisions, the port base) is stored sc1, drained before the signalling
-// atomic and loaded sc1, on lines no workgroup reads with a plain load in
-// the launch (MI355X_MICROARCH.md, inter-workgroup visibility); the flag is
-// polled with a compare-exchange.  Everything else was written by an earlier
-// launch.  With nothing deferred (the steady state) the grid exits at once.
-// state (128-B line 0): [0] NEXT_PORT [1] entries; by call parity p:
-// [4+p] deferred packets [6+p] tickets [9+p] phase-1 chunks done [14+p]
-// tag collisions (the other parity is the previous call's, cleared here
-// for the next one).  The words handed over inside the launch sit on line
-// 1, which nothing reads with a plain load (every workgroup reads line 0
-// plainly, so its L2 holds it): [32] the port base of the batch in flight,
-// [33+p] the phase-2 flag, [36] repair mode.
+// joined a slot on its claim tag alone in the stash.  Two launches of nb
+// workgroups (nb = chunks of kBlock packets), one chunk each:
+//   nat64_tail_order     each tag-joined packet's key is compared with its
+//                        slot's key words (a tag collision is listed for the
+//                        repair below), and the packets that are a new key's
+//                        first packet (w[7] == i) give a 256-bit mask and a
+//                        count per chunk; the workgroup that arrives last
+//                        (arrivals counted in 32 shards of their own lines,
+//                        then one counter: an atomic on one word serializes
+//                        at its memory-side unit, ~90 per us) repairs any
+//                        collisions, scans the counts into each chunk's
+//                        base ordinal and advances NEXT_PORT;
+//   nat64_tail_patch     every deferred packet computes its key's port from
+//                        the first packet's chunk base and mask -- no hand-off
+//                        between packets of one key -- and patches its frame
+//                        (the fused kernel wrote it with source port 0); a
+//                        first packet also commits the key (port, kPersist,
+//                        ADDR_MAP).
+// Inside nat64_tail_order, the counts and the collision list are stored sc1,
+// drained before the arrival atomics and loaded sc1 by the last workgroup
+// (MI355X_MICROARCH.md, inter-workgroup visibility: the last arriver, told by
+// its add); everything else crosses a launch boundary.  With nothing
+// deferred (the steady state) both grids return at once.
+// state (line 0): [0] NEXT_PORT [1] entries [4+p] the batch has deferred
+// frames (p = call parity; the previous call's flag is cleared by this
+// call's order launch).  The arrival counters, the collision count and the
+// port base live in the scratch (TailCtl), zeroed again by the last arriver.
 __device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
   return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-constexpr uint32_t kStBase = 32u, kStFlag = 33u, kStMode = 36u;  // state line 1
-constexpr uint32_t kStMism = 14u;                                  // state line 0, by parity
+__device__ __forceinline__ uint32_t add_agent(uint32_t *p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The tail's control words in the scratch, after the chunk arrays and the
+// collision list: 32 arrival shards (one 128-B line each), then a line with
+// the shard-completion counter, the collision count and the port base.
+constexpr uint32_t kShards = 32u, kLineW = 32u;
+struct TailCtl {
+  uint32_t *shard;  // [kShards * kLineW]: shard s counts at shard[s * kLineW]
+  uint32_t *top;    // [0] shards complete, [1] collisions, [2] port base
+};
+__device__ __forceinline__ TailCtl tail_ctl(const Nat64Args &a) {
+  return TailCtl{a.ctl, a.ctl + kShards * kLineW};
+}
 
 // Whether packet i's stashed key is its slot's key (w = the slot's words).
 __device__ __forceinline__ bool stash_matches(const Nat64Args &a, uint32_t i, const uint32_t *w) {
@@ -1168,14 +1183,13 @@ __device__ __forceinline__ bool stash_matches(const Nat64Args &a, uint32_t i, co
          (uint32_t)a.stash_port[i] == (w[6] & 0xffffu);
 }
 
-// Phase 1 of chunk c (all kBlock threads): the chunk's first-packet mask
-// words and count, sc1.  Tag-joined packets whose key is not their slot's
-// (collisions) go to the list `mism` (an sc1 entry per packet, counted in
-// state[kStMism + p]); they are never a first packet here.
+// One chunk's first packets (all kBlock threads): the mask words and the
+// count, sc1.  Tag-joined packets whose key is not their slot's (collisions)
+// go to the list `mism` (sc1 entries, counted in ctl.top[1]); they are never
+// a first packet here.
 __device__ __forceinline__ void chunk_firsts(const Nat64Args &a, uint32_t c, bool verify,
                                              uint32_t *cnt, uint32_t *cmask, uint32_t *mism,
-                                             uint32_t *s_part) {
-  uint32_t *const st = a.pm.state;
+                                             const TailCtl &ctl) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t i = c * kBlock + threadIdx.x;
   const uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
@@ -1193,30 +1207,27 @@ __device__ __forceinline__ void chunk_firsts(const Nat64Args &a, uint32_t c, boo
   }
   const uint64_t bm = __ballot(bad);
   if (bm) {  // rare: list the wave's collisions
+    const uint32_t first = (uint32_t)__builtin_ctzll(bm);
     uint32_t at = 0;
-    if (lane == (uint32_t)__builtin_ctzll(bm))
-      at = __hip_atomic_fetch_add(&st[kStMism + a.par], (uint32_t)__popcll(bm), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-    at = __shfl(at, (int)__builtin_ctzll(bm));
+    if (lane == first) at = add_agent(&ctl.top[1], (uint32_t)__popcll(bm));
+    at = __shfl(at, (int)first);
     if (bad) st_sc1(&mism[at + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))], i);
   }
   const uint32_t n_first = (uint32_t)__syncthreads_count(f);
   if (threadIdx.x == 0) st_sc1(&cnt[c], n_first);
-  (void)s_part;
 }
 
 // The repair of tag collisions (rare: distinct keys whose claim tags are
-// equal met in a probe chain), by the last phase-1 workgroup: each listed
-// packet looks its key up exactly (its slot's key words were written by the
-// fused kernel; slots this repair claims, by this workgroup) and joins that
-// slot, claims a new one, or takes a committed key's port; the first packet
-// of every slot a colliding packet had joined is recomputed (a collision may
-// have lowered it), and the chunks whose first packets may have changed are
-// counted again.  Phase 2 then reads what the repair may have changed with
-// compare-exchanges (repair mode).
-constexpr uint32_t kRepairSet = 256;  // slots / chunks per pass
+// equal met in a probe chain), by the last arriver: each listed packet looks
+// its key up exactly (its slot's key words were written by the fused kernel;
+// slots this repair claims, by this workgroup) and joins that slot or claims
+// a new one; the first packet of every slot a colliding packet had joined is
+// recomputed (a collision may have lowered it), and the chunks whose first
+// packets may have changed are counted again.  The patch launch reads the
+// result behind the launch boundary.
+constexpr uint32_t kRepairSet = 256;  // wrong slots per pass
 __device__ void tail_repair(const Nat64Args &a, uint32_t nb, uint32_t nmism, const uint32_t *mism,
-                            uint32_t *cnt, uint32_t *cmask, uint32_t *s_part) {
+                            uint32_t *cnt, uint32_t *cmask, const TailCtl &ctl) {
   __shared__ uint32_t s_slot[kRepairSet], s_min[kRepairSet], s_chunk[4 * kRepairSet];
   __shared__ uint32_t s_ns, s_nc, s_all;
   if (threadIdx.x == 0) {
@@ -1289,7 +1300,7 @@ __device__ void tail_repair(const Nat64Args &a, uint32_t nb, uint32_t nmism, con
   }
   __syncthreads();
   // 2. the first packet of each slot a collision had joined: the minimum
-  // over the packets that belong to it now (passes of kRepairSet slots)
+  // over the packets that belong to it now
   const uint32_t ns = s_ns;
   for (uint32_t i = threadIdx.x; i < a.n; i += kBlock) {
     const uint32_t ps = a.pkt_slot[i];
@@ -1311,22 +1322,18 @@ __device__ void tail_repair(const Nat64Args &a, uint32_t nb, uint32_t nmism, con
       }
     }
   __syncthreads();
-  // (a second pass for more than kRepairSet wrong slots)
   // 3. count the affected chunks again (every chunk when the sets overflowed)
   const uint32_t nc = s_all ? nb : s_nc;
-  for (uint32_t q = 0; q < nc; ++q) {
-    const uint32_t c = s_all ? q : s_chunk[q];
-    chunk_firsts(a, c, false, cnt, cmask, nullptr, s_part);
-  }
-  if (threadIdx.x == 0) st_sc1(&a.pm.state[kStMode], 1u);
+  for (uint32_t q = 0; q < nc; ++q) chunk_firsts(a, s_all ? q : s_chunk[q], false, cnt, cmask, nullptr, ctl);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
 }
 
-// The last phase-1 workgroup: exclusive scan of the chunk counts into the
-// chunk bases, the port base, NEXT_PORT advanced (AtomicU16 wrap), the flag.
+// The last arriver: exclusive scan of the chunk counts into the chunk bases
+// (read by the patch launch), the port base, NEXT_PORT advanced (AtomicU16
+// wrap), and the control words zeroed for the next call.
 __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const uint32_t *cnt,
-                                          uint32_t *cbase, uint32_t *s_part) {
+                                          uint32_t *cbase, const TailCtl &ctl, uint32_t *s_part) {
   uint32_t *const st = a.pm.state;
   const uint32_t per = (nb + kBlock - 1u) / kBlock;
   const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
@@ -1334,7 +1341,7 @@ __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const
   for (uint32_t b = b0; b < b1; ++b) sum += ld_sc1(&cnt[b]);
   s_part[threadIdx.x] = sum;
   __syncthreads();
-  if (threadIdx.x == 0) {  // 256 partial sums: one thread (the scan of a few thousand counts)
+  if (threadIdx.x == 0) {  // 256 partial sums: one thread
     uint32_t run = 0;
     for (uint32_t t = 0; t < kBlock; ++t) {
       const uint32_t x = s_part[t];
@@ -1347,134 +1354,114 @@ __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const
   uint32_t run = s_part[threadIdx.x];
   for (uint32_t b = b0; b < b1; ++b) {
     const uint32_t c = ld_sc1(&cnt[b]);
-    st_sc1(&cbase[b], run);
+    cbase[b] = run;
     run += c;
   }
+  if (threadIdx.x < kShards) ctl.shard[threadIdx.x * kLineW] = 0u;
   if (threadIdx.x == 0) {
     const uint32_t total = s_part[kBlock], base = st[0];
-    st_sc1(&st[kStBase], base);
+    ctl.top[0] = 0u;
+    ctl.top[1] = 0u;
+    ctl.top[2] = base;
     st[0] = (base + total) & 0xffffu;  // read by the next call's launches
     st[1] += total;
   }
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (threadIdx.x == 0) st_sc1(&st[kStFlag + a.par], 1u);
 }
 
-__device__ __forceinline__ uint32_t rd_cas(uint32_t *p) { return atomicCAS(p, 0u, 0u); }
+__device__ __forceinline__ uint32_t shard_size(uint32_t nb, uint32_t s) {
+  return s < nb ? (nb - s + kShards - 1u) / kShards : 0u;
+}
 
-__global__ __launch_bounds__(kBlock) void nat64_tail(Nat64Args a, uint32_t nb) {
-  __shared__ uint32_t s_ticket, s_last;
+__global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t nb) {
+  __shared__ uint32_t s_last, s_nm;
   __shared__ uint32_t s_part[kBlock + 1];
   uint32_t *const st = a.pm.state;
-  const uint32_t p = a.par;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the previous call's counters, for the next call
-    st[4u + (p ^ 1u)] = 0u;
-    st[6u + (p ^ 1u)] = 0u;
-    st[9u + (p ^ 1u)] = 0u;
-    st[kStMism + (p ^ 1u)] = 0u;
-    st[kStFlag + (p ^ 1u)] = 0u;
-  }
-  if (st[4u + p] == 0u) return;  // nothing deferred: no new key
+  if (blockIdx.x == 0 && threadIdx.x == 0) st[4u + (a.par ^ 1u)] = 0u;  // the previous call's flag
+  if (st[4u + a.par] == 0u) return;  // nothing deferred: no new key
   uint32_t *const cnt = a.chunks, *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
   uint32_t *const mism = a.chunks + 10u * nb;  // the tag collisions (packet indices)
-  for (;;) {
-    if (threadIdx.x == 0) s_ticket = atomicAdd(&st[6u + p], 1u);
-    __syncthreads();
-    const uint32_t t = s_ticket;
-    if (t >= 2u * nb) return;  // workgroup-uniform
-    if (t < nb) {
-      chunk_firsts(a, t, CGPU_NAT64_TAGJOIN != 0, cnt, cmask, mism, s_part);
-      __builtin_amdgcn_s_waitcnt(0);  // every storing wave drains before the arrival
-      __syncthreads();
-      if (threadIdx.x == 0)
-        s_last = __hip_atomic_fetch_add(&st[9u + p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1u;
-      __syncthreads();
-      if (s_last) {  // the workgroup that completed phase 1 last
-        __shared__ uint32_t s_nm;
-        if (threadIdx.x == 0) {
-          s_nm = rd_cas(&st[kStMism + p]);
-          st_sc1(&st[kStMode], 0u);
-        }
-        __syncthreads();
-        if (s_nm) tail_repair(a, nb, s_nm, mism, cnt, cmask, s_part);
-        tail_scan(a, nb, cnt, cbase, s_part);
-      }
-      __syncthreads();  // s_ticket, s_last, s_part are rewritten next round
-      continue;
+  const TailCtl ctl = tail_ctl(a);
+  const uint32_t c = blockIdx.x;
+  chunk_firsts(a, c, CGPU_NAT64_TAGJOIN != 0, cnt, cmask, mism, ctl);
+  __builtin_amdgcn_s_waitcnt(0);  // every storing wave drains before the arrival
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // arrival: the shard of this chunk, then (its last arriver) the shard count
+    const uint32_t s = c % kShards;
+    bool last = false;
+    if (add_agent(&ctl.shard[s * kLineW], 1u) == shard_size(nb, s) - 1u) {
+      const uint32_t used = nb < kShards ? nb : kShards;
+      last = add_agent(&ctl.top[0], 1u) == used - 1u;
     }
-    // phase 2: chunk t - nb, once every chunk base is known (the flag is
-    // polled with a compare-exchange, performed at the coherence point)
-    __shared__ uint32_t s_base, s_mode;
-    if (threadIdx.x == 0) {
-      // (bounded, ~2 s: a wait that never ended would mean a broken
-      // protocol; the results are then wrong, but the GPU is not hung)
-      for (uint32_t spin = 0; rd_cas(&st[kStFlag + p]) == 0u && spin < (1u << 24); ++spin)
-        __builtin_amdgcn_s_sleep(2);
-      s_base = ld_sc1(&st[kStBase]);
-      s_mode = ld_sc1(&st[kStMode]);
-    }
-    __syncthreads();
-    const uint32_t port_base = s_base;
-    const bool repaired = s_mode != 0u;  // the repair may have changed pkt_slot and slot words
-    const uint32_t i = (t - nb) * kBlock + threadIdx.x;
-    uint32_t ps = kNoSlot;
-    if (i < a.n) ps = repaired ? rd_cas(&a.pkt_slot[i]) : a.pkt_slot[i];
-    if (ps != kNoSlot && (ps & (kLocalBit | kPatchBit))) {
-      uint32_t *w = a.pm.slots[ps & kSlotMask].w;
-      uint32_t port;
-      if (ps & kLocalBit) {
-        const uint32_t fi = repaired ? rd_cas(&w[7]) : w[7];  // the key's first packet
-        const uint32_t fc = fi / kBlock, fb = fi % kBlock;
-        uint32_t below = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j) {
-          const uint32_t mw = ld_sc1(&cmask[8u * fc + j]);
-          const uint32_t lo = 32u * j;
-          below += (uint32_t)__builtin_popcount(fb >= lo + 32u ? mw : (fb > lo ? mw & ((1u << (fb - lo)) - 1u) : 0u));
-        }
-        const uint32_t ordinal = ld_sc1(&cbase[fc]) + below;
-        port = (port_base + ordinal) & 0xffffu;  // NEXT_PORT.fetch_add order
-        if (fi == i) {
-          uint32_t kw[5];
-#pragma unroll
-          for (int j = 0; j < 5; ++j) kw[j] = repaired ? rd_cas(&w[2 + j]) : w[2 + j];
-          // ADDR_MAP.insert_new(port, key) (main.rs:50): the first mapping of
-          // a port wins, also after NEXT_PORT wraps.  This call's ordinals o
-          // and o + 65536k share a port, so only its first lap (o < 65536)
-          // can be first, and only if no earlier call mapped the port: one
-          // writer per entry, no race.
-          uint32_t *e = a.pm.rev + 5u * port;
-          if (ordinal < 65536u && !(e[4] & kRevValid)) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) e[j] = kw[j];
-            e[4] = (kw[4] & 0xffffu) | kRevValid;
-          }
-          // PORT_MAP.insert_new (main.rs:49): the key, committed for later batches
-          w[6] = (kw[4] & 0xffffu) | (port << 16);
-          w[0] = kPersist;
-        }
-      } else {  // (repair) a committed key found for a colliding packet
-        port = rd_cas(&w[6]) >> 16;
-      }
-      // The frame was written with source port 0 and the checksum c0 of
-      // that frame; set the port and patch the checksum, ~fold(~c0 + port)
-      // -- exact: the sum behind c0 includes the pseudo-header's protocol 6,
-      // so it is never 0 and ~c0 recovers its fold.
-      uint8_t *o = a.out_arena + a.out_off[i];
-      // the VLAN depth from the output's Ethernet header (the input's own)
-      const uint32_t marker = ((uint32_t)o[12] << 8) | o[13];
-      const uint32_t k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
-      uint8_t *tcp = o + 34u + 4u * k;  // the TCP header
-      const uint32_t c0 = ((uint32_t)tcp[16] << 8) | tcp[17];
-      const uint32_t c = (~fold32(((~c0) & 0xffffu) + port)) & 0xffffu;
-      tcp[0] = (uint8_t)(port >> 8);
-      tcp[1] = (uint8_t)port;
-      tcp[16] = (uint8_t)(c >> 8);
-      tcp[17] = (uint8_t)c;
-    }
-    __syncthreads();  // s_ticket, s_base, s_mode are rewritten next round
+    s_last = last;
   }
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) s_nm = atomicCAS(&ctl.top[1], 0u, 0u);  // the collisions, read at the coherence point
+  __syncthreads();
+  if (s_nm) tail_repair(a, nb, s_nm, mism, cnt, cmask, ctl);
+  tail_scan(a, nb, cnt, cbase, ctl, s_part);
+}
+
+__global__ __launch_bounds__(kBlock) void nat64_tail_patch(Nat64Args a, uint32_t nb) {
+  if (a.pm.state[4u + a.par] == 0u) return;  // nothing deferred: no new key
+  const uint32_t *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
+  const TailCtl ctl = tail_ctl(a);
+  const uint32_t port_base = ctl.top[2];
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
+  if (ps == kNoSlot || !(ps & (kLocalBit | kPatchBit))) return;
+  uint32_t *w = a.pm.slots[ps & kSlotMask].w;
+  uint32_t port;
+  if (ps & kLocalBit) {
+    const uint32_t fi = w[7];  // the key's first packet
+    const uint32_t fc = fi / kBlock, fb = fi % kBlock;
+    const u32x4 m0 = *reinterpret_cast<const u32x4 *>(cmask + 8u * fc);
+    const u32x4 m1 = *reinterpret_cast<const u32x4 *>(cmask + 8u * fc + 4u);
+    const uint32_t mw[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
+    uint32_t below = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8u; ++j) {
+      const uint32_t lo = 32u * j;
+      below += (uint32_t)__builtin_popcount(fb >= lo + 32u ? mw[j] : (fb > lo ? mw[j] & ((1u << (fb - lo)) - 1u) : 0u));
+    }
+    const uint32_t ordinal = cbase[fc] + below;
+    port = (port_base + ordinal) & 0xffffu;  // NEXT_PORT.fetch_add order
+    if (fi == i) {
+      const uint32_t kw[5] = {w[2], w[3], w[4], w[5], w[6]};
+      // ADDR_MAP.insert_new(port, key) (main.rs:50): the first mapping of a
+      // port wins, also after NEXT_PORT wraps.  This call's ordinals o and
+      // o + 65536k share a port, so only its first lap (o < 65536) can be
+      // first, and only if no earlier call mapped the port: one writer per
+      // entry, no race.
+      uint32_t *e = a.pm.rev + 5u * port;
+      if (ordinal < 65536u && !(e[4] & kRevValid)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[j] = kw[j];
+        e[4] = (kw[4] & 0xffffu) | kRevValid;
+      }
+      // PORT_MAP.insert_new (main.rs:49): the key, committed for later batches
+      w[6] = (kw[4] & 0xffffu) | (port << 16);
+      w[0] = kPersist;
+    }
+  } else {  // (repair) a committed key found for a colliding packet
+    port = w[6] >> 16;
+  }
+  // The frame was written with source port 0 and the checksum c0 of that
+  // frame; set the port and patch the checksum, ~fold(~c0 + port) -- exact:
+  // the sum behind c0 includes the pseudo-header's protocol 6, so it is
+  // never 0 and ~c0 recovers its fold.
+  uint8_t *o = a.out_arena + a.out_off[i];
+  // the VLAN depth from the output's Ethernet header (the input's own)
+  const uint32_t marker = ((uint32_t)o[12] << 8) | o[13];
+  const uint32_t k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
+  uint8_t *tcp = o + 34u + 4u * k;  // the TCP header
+  const uint32_t c0 = ((uint32_t)tcp[16] << 8) | tcp[17];
+  const uint32_t c = (~fold32(((~c0) & 0xffffu) + port)) & 0xffffu;
+  tcp[0] = (uint8_t)(port >> 8);
+  tcp[1] = (uint8_t)port;
+  tcp[16] = (uint8_t)(c >> 8);
+  tcp[17] = (uint8_t)c;
 }
 
 // ============================ 4to6 direction =================================
@@ -1822,8 +1809,7 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
   }
   if (i == 0) {
     pm.state[0] = first_port;  // NEXT_PORT
-    // entries, the port base, and the per-call-parity counters of the tail
-    // (deferred packets, tickets, phase-1 chunks done, phase-2 flag)
+    // entries and the per-call-parity deferred flags
     for (uint32_t j = 1; j < 64u; ++j) pm.state[j] = 0u;
   }
 }
@@ -1831,11 +1817,10 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
 }  // namespace
 
 uint32_t nat64_num_blocks(uint32_t n) { return (n + kBlock - 1) / kBlock; }
-
-#ifndef CGPU_NAT64_TAIL_GRID
-#define CGPU_NAT64_TAIL_GRID 2048
-#endif
-constexpr uint32_t kTailGrid = CGPU_NAT64_TAIL_GRID;  // most workgroups of the tail kernel
+size_t nat64_ctl_offset(uint32_t n) {
+  return 4ull * (10ull * nat64_num_blocks(n) + ((n + kLineW - 1u) / kLineW) * kLineW);
+}
+size_t nat64_chunk_bytes(uint32_t n) { return nat64_ctl_offset(n) + 4ull * (kShards + 1u) * kLineW; }
 
 hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStream_t s) {
   // one thread per slot and ADDR_MAP entry
@@ -1853,10 +1838,10 @@ hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s, hipEvent_t done)
   const uint32_t fpb = (kBlock / 64u) * kRowFrames;  // fused: kRowFrames frames per wave
   const uint32_t nbf = (a.n + fpb - 1) / fpb;
   hipLaunchKernelGGL(nat64_6to4_fused, dim3(nbf), dim3(kBlock), 0, s, a);
-  // the tail (order + the deferred frames' ports) takes 2 nb tickets; in the
-  // steady state (no new key) it returns at once
-  const uint32_t tg = 2u * nb < kTailGrid ? 2u * nb : kTailGrid;
-  hipExtLaunchKernelGGL(nat64_tail, dim3(tg), dim3(kBlock), 0, s, nullptr, done, 0, a, nb);
+  // the tail: the order of the new keys, then their frames' ports; in the
+  // steady state (no new key) both grids return at once
+  hipLaunchKernelGGL(nat64_tail_order, dim3(nb), dim3(kBlock), 0, s, a, nb);
+  hipExtLaunchKernelGGL(nat64_tail_patch, dim3(nb), dim3(kBlock), 0, s, nullptr, done, 0, a, nb);
   return hipGetLastError();
 }
 
