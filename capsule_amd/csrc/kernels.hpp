@@ -40,13 +40,12 @@ hipError_t launch_reconcile(const ParseArgs &a, hipStream_t s);
 // Device port map (examples/nat64/main.rs:37-53): open addressing, linear
 // probing over 32-byte slots (PortSlot).  A slot's ref word is 0 (empty),
 // kPersist (committed; its key words are valid) or (packet index + 1) of the
-// packet of the batch in flight that claimed it (| kReady once its key words
-// are published).
+// packet of the batch in flight that claimed it.
 constexpr uint32_t kPersist = 0x80000000u;
 
 // One slot of the device port map, 32 bytes (two dwordx4, one cache line
 // half): a lookup is a single line.
-//   w[0] ref   0 empty | kPersist committed | (claiming packet + 1) [| kReady]
+//   w[0] ref   0 empty | kPersist committed | (claiming packet + 1)
 //   w[1]       claim tag (a second hash of the key; w[0..1] are one 64-bit CAS)
 //   w[2..5]    key: v6 source address (wire bytes as LE dwords)
 //   w[6]       key: v6-side TCP source port | assigned gateway port << 16
@@ -96,6 +95,7 @@ struct Nat64Args {
                          // scratch's capacity, not the call's n: zeroed once)
   u32x4 *stash_key;      // scratch [n]: a tag-joined packet's key (v6 source address) ...
   uint16_t *stash_port;  // scratch [n]: ... and its TCP source port, verified by the tail
+  uint32_t *stash_c0;    // scratch [n]: a deferred frame's TCP checksum (port 0) | VLAN depth << 16
   uint32_t par;          // call parity: selects the deferred flag state[4 + par]
   uint32_t room;         // data room of Mbuf::extend's tailroom model (mbuf.rs:225-233):
                          // 2048 for device batches; 65535 on the mbuf path, whose

@@ -63,10 +63,6 @@ constexpr uint32_t kLocalBit = 0x40000000u;  // pkt_slot: key first seen in this
 constexpr uint32_t kClaimBit = 0x20000000u;  // pkt_slot: this packet claimed the slot
 constexpr uint32_t kPatchBit = 0x80000000u;  // pkt_slot (tail repair): a committed key's port
 constexpr uint32_t kSlotMask = 0x1fffffffu;  // slot index (capacity_log2 <= 29)
-#ifndef CGPU_NAT64_TAGJOIN  // 1: joins on the claim tag, verified by the tail; 0: verified in the probe
-#define CGPU_NAT64_TAGJOIN 1
-#endif
-[[maybe_unused]] constexpr uint32_t kReady = 0x40000000u;  // ref (in-kernel verify): key words published
 constexpr uint32_t kV4Addr = 0x017100cbu;    // 203.0.113.1 as LE dword of wire bytes
 // The tailroom model of Mbuf::extend (mbuf.rs:225-233) is Nat64Args::room:
 // RTE_MBUF_DEFAULT_DATAROOM = 2048 for device batches; on the mbuf path the
@@ -270,30 +266,20 @@ __device__ __forceinline__ void ipv4_header(const V6 &v, uint32_t len, uint32_t 
 // packet index recorded (atomicMin) for the tail kernel.
 //
 // A claim is one 64-bit CAS of {ref = i + 1, tag} into an empty slot; the
-// claimer then publishes the key words with atomic exchanges and, once they
-// have returned, sets kReady in ref with an atomic OR.  A packet that finds
-// a batch-local claim with its own tag waits for kReady and compares the
-// key words, both read with atomic RMWs (an OR of 0): atomics are performed
-// at the memory-side coherence point, so no XCD's L2 can serve them a stale
-// copy of the slot line (its own earlier probe load cached one: plain or
-// sc1 reads of the words published in this launch would read it,
-// MI355X_MICROARCH.md, inter-workgroup visibility).  The claimer never waits
-// between its CAS and the publish, so the wait ends.  A different tag is a
-// different key: no read, next slot.  Keys committed by earlier batches are
-// matched from the 32-B slot load (their words were written by an earlier
-// launch).  refs only ever go 0 -> (i + 1) -> (i + 1) | kReady -> kPersist,
-// and a claim's tag never changes, so a stale probe load at worst leads to
-// the CAS, which returns the coherent word.
-// (An idempotent OR / ADD would be compiled into an sc1 load, which the L2
-// serves; a compare-exchange of 0 with 0 is performed at the coherence point
-// and leaves the word as it is.)
-__device__ __forceinline__ uint32_t rd_atomic(uint32_t *p) {
-  return atomicCAS(p, 0u, 0u);
-}
-__device__ __forceinline__ uint64_t rd_atomic64(uint32_t *p) {
-  return atomicCAS(reinterpret_cast<unsigned long long *>(p), 0ull, 0ull);
-}
-
+// claimer then writes the key words (plain stores: nothing in this launch
+// reads them) and its index into w[7].  A packet that finds a batch-local
+// claim with its own tag joins it on the tag alone: it stashes its key, and
+// the tail compares the stash with the slot's key words behind the kernel
+// boundary, where they are coherent, and repairs the rare collision (two
+// keys of one tag in one probe chain).  No lane waits for another: a wait on
+// a claimer's publish would need the key words read at the coherence point
+// (atomics; plain and sc1 loads can be served a stale copy of the slot line
+// by the XCD's L2, which this lane's own probe load filled), and costs more
+// than the stash.  A different tag is a different key: next slot.  Keys
+// committed by earlier batches are matched from the 32-B slot load (their
+// words were written by an earlier launch).  refs only ever go 0 -> (i + 1)
+// -> kPersist, and a claim's tag never changes, so a stale probe load at
+// worst leads to the CAS, which returns the coherent word.
 __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i,
                                                   const uint32_t (&key)[5], uint32_t h, u32x4 s0,
                                                   u32x4 s1, uint32_t &port) {
@@ -307,37 +293,20 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
     }
     uint32_t *w = a.pm.slots[h].w;
     uint32_t ref = s0[0], stag = s0[1];
-    bool claimed = false;
     if (ref == 0u) {
       const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long *>(w), 0ull,
                                                (unsigned long long)(i + 1u) |
                                                    ((unsigned long long)tag << 32));
-      claimed = old == 0ull;
+      if (old == 0ull) {  // claimed: the key words, read behind the kernel boundary only
+        *reinterpret_cast<u32x2 *>(&w[2]) = u32x2{key[0], key[1]};
+        *reinterpret_cast<u32x2 *>(&w[4]) = u32x2{key[2], key[3]};
+        w[6] = key[4];
+        atomicMin(&w[7], i);
+        return h | kLocalBit | kClaimBit;
+      }
       ref = (uint32_t)old;
       stag = (uint32_t)(old >> 32);
     }
-    // Every claimer of the wave publishes before any lane of the wave waits
-    // for a publish (the fences keep the compiler from sinking the publish
-    // below the wait).
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (claimed) {
-#if CGPU_NAT64_TAGJOIN
-      // the key words are read behind the kernel boundary only
-      *reinterpret_cast<u32x2 *>(&w[2]) = u32x2{key[0], key[1]};
-      *reinterpret_cast<u32x2 *>(&w[4]) = u32x2{key[2], key[3]};
-      w[6] = key[4];
-#else
-#pragma unroll
-      for (int j = 0; j < 5; ++j)
-        (void)__hip_atomic_exchange(&w[2 + j], key[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // the exchanges are performed before the flag
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      (void)__hip_atomic_fetch_or(&w[0], kReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-      atomicMin(&w[7], i);
-      return h | kLocalBit | kClaimBit;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (ref & kPersist) {
       const uint32_t other[5] = {s0[2], s0[3], s1[0], s1[1], s1[2] & 0xffffu};
       if (key_eq(key, other)) {
@@ -345,34 +314,13 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
         return h;
       }
     } else if (stag == tag) {
-#if CGPU_NAT64_TAGJOIN
-      // joined on the tag alone: the key goes to the stash, and the tail
-      // compares it with the slot's key words behind the kernel boundary
-      // (a tag collision is repaired there)
+      // joined on the tag alone: the key goes to the stash; the key's first
+      // packet index (w[7] only decreases, so a value loaded with the slot
+      // that is already below i makes the atomic moot)
       a.stash_key[i] = u32x4{key[0], key[1], key[2], key[3]};
       a.stash_port[i] = (uint16_t)key[4];
       if (s1[3] > i) atomicMin(&w[7], i);
       return h | kLocalBit;
-#elif defined(CGPU_NAT64_ABL_NOREP)  // timing ablation only: tags trusted, no key compare
-      const bool match = true;
-#else
-      for (uint32_t spin = 0; !(ref & kReady) && spin < (1u << 22); ++spin) {
-        __builtin_amdgcn_s_sleep(1);
-        ref = rd_atomic(&w[0]);
-      }
-      const uint64_t k01 = rd_atomic64(&w[2]), k23 = rd_atomic64(&w[4]);
-      const uint32_t other[5] = {(uint32_t)k01, (uint32_t)(k01 >> 32), (uint32_t)k23,
-                                 (uint32_t)(k23 >> 32), rd_atomic(&w[6])};
-      const bool match = key_eq(key, other);
-#endif
-#if !CGPU_NAT64_TAGJOIN
-      if (match) {
-        // the key's first packet index (w[7] only decreases, so a value
-        // loaded with the slot that is already below i makes the atomic moot)
-        if (s1[3] > i) atomicMin(&w[7], i);
-        return h | kLocalBit;
-      }
-#endif
     }
     h = (h + 1u) & a.pm.cap_mask;
   }
@@ -396,6 +344,8 @@ struct FrameRec {
   uint32_t in_off, o_off, new_len, info;
   uint32_t V[10];
   uint32_t ph;
+  uint32_t defer_i;  // 6to4: the packet index of a deferred frame (its checksum is
+                     // stashed for the tail), else kNoSlot
 };
 
 // Output dword at header-relative position r (frame dword - VLAN depth) in
@@ -520,6 +470,7 @@ __device__ __forceinline__ void finish_frame(const Nat64Args &a, rsrc_t ors, con
     const uint32_t span = (nl - (54u + 4u * k)) & 0xffffu;
     tcp_c = (~fold32(swap16(fold32(acc + f.ph)) + span + 6u)) & 0xffffu;
   }
+  if (TO4 && f.defer_i != kNoSlot) a.stash_c0[f.defer_i] = tcp_c | (k << 16);
   const uint32_t tw = TO4 ? k : k + 1u;  // dword of the checksum field in the held chunk
 #pragma unroll
   for (uint32_t t = 0; t < 4u; ++t)
@@ -837,6 +788,7 @@ __device__ __forceinline__ void quad_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
 #pragma unroll
     for (int j = 5; j < 10; ++j) f.V[j] = 0u;
     f.ph = 0u;
+    f.defer_i = deferred ? d.i : kNoSlot;
     rewrite_quad<true>(a, rs, ors, g, d, al16, f, X, E);
   }
 #endif
@@ -1101,6 +1053,8 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     const uint32_t payload = rec[17];
     *reinterpret_cast<u32x4 *>(rec + 16) =
         u32x4{act ? nl : 0u, payload + accA, ph | (k << 16), o_off};
+    // a deferred frame's checksum (with port 0) and VLAN depth, for the tail
+    if (deferred) a.stash_c0[i] = ((~fold32(ph + swap16(fold32(payload + accA)))) & 0xffffu) | (k << 16);
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #ifndef CGPU_NAT64_ABL_NOREWRITE
@@ -1145,11 +1099,17 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a
 //                        (the fused kernel wrote it with source port 0); a
 //                        first packet also commits the key (port, kPersist,
 //                        ADDR_MAP).
-// Inside nat64_tail_order, the counts and the collision list are stored sc1,
+// Both are grid-stride loops over the chunks on grids of at most kOrderGrid
+// / kPatchGrid workgroups: in the steady state each workgroup only reads
+// the flag and returns, so the grid's size is the launch's cost.  Inside
+// nat64_tail_order, the counts and the collision list are stored sc1,
 // drained before the arrival atomics and loaded sc1 by the last workgroup
-// (MI355X_MICROARCH.md, inter-workgroup visibility: the last arriver, told by
-// its add); everything else crosses a launch boundary.  With nothing
-// deferred (the steady state) both grids return at once.
+// (MI355X_MICROARCH.md, inter-workgroup visibility: the last arriver, told
+// by its add); everything else crosses a launch boundary.  The arrivals are
+// counted per XCD (blockIdx % 8 under round-robin placement, a speed choice
+// only), on counters 4 KiB apart, then the XCD counts on one: atomics on one
+// line, and on lines 128 B apart, serialized at ~13 ns each (4096
+// workgroups arriving on 32 counters 128 B apart took 48 us).
 // state (line 0): [0] NEXT_PORT [1] entries [4+p] the batch has deferred
 // frames (p = call parity; the previous call's flag is cleared by this
 // call's order launch).  The arrival counters, the collision count and the
@@ -1164,16 +1124,17 @@ __device__ __forceinline__ uint32_t add_agent(uint32_t *p, uint32_t v) {
   return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The tail's control words in the scratch, after the chunk arrays and the
-// collision list: 32 arrival shards (one 128-B line each), then a line with
-// the shard-completion counter, the collision count and the port base.
-constexpr uint32_t kShards = 32u, kLineW = 32u;
+// The tail's control words in the scratch: 8 arrival shards 4 KiB apart,
+// then a line with the shard-completion counter, the collision count and
+// the port base.
+constexpr uint32_t kShards = 8u, kShardW = 1024u;
+constexpr uint32_t kOrderGrid = 256u, kPatchGrid = 1024u;
 struct TailCtl {
-  uint32_t *shard;  // [kShards * kLineW]: shard s counts at shard[s * kLineW]
+  uint32_t *shard;  // [kShards * kShardW]: shard s counts at shard[s * kShardW]
   uint32_t *top;    // [0] shards complete, [1] collisions, [2] port base
 };
 __device__ __forceinline__ TailCtl tail_ctl(const Nat64Args &a) {
-  return TailCtl{a.ctl, a.ctl + kShards * kLineW};
+  return TailCtl{a.ctl, a.ctl + kShards * kShardW};
 }
 
 // Whether packet i's stashed key is its slot's key (w = the slot's words).
@@ -1357,7 +1318,7 @@ __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const
     cbase[b] = run;
     run += c;
   }
-  if (threadIdx.x < kShards) ctl.shard[threadIdx.x * kLineW] = 0u;
+  if (threadIdx.x < kShards) ctl.shard[threadIdx.x * kShardW] = 0u;
   if (threadIdx.x == 0) {
     const uint32_t total = s_part[kBlock], base = st[0];
     ctl.top[0] = 0u;
@@ -1368,8 +1329,8 @@ __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const
   }
 }
 
-__device__ __forceinline__ uint32_t shard_size(uint32_t nb, uint32_t s) {
-  return s < nb ? (nb - s + kShards - 1u) / kShards : 0u;
+__device__ __forceinline__ uint32_t shard_size(uint32_t grid, uint32_t s) {
+  return s < grid ? (grid - s + kShards - 1u) / kShards : 0u;
 }
 
 __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t nb) {
@@ -1381,16 +1342,16 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   uint32_t *const cnt = a.chunks, *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
   uint32_t *const mism = a.chunks + 10u * nb;  // the tag collisions (packet indices)
   const TailCtl ctl = tail_ctl(a);
-  const uint32_t c = blockIdx.x;
-  chunk_firsts(a, c, CGPU_NAT64_TAGJOIN != 0, cnt, cmask, mism, ctl);
+  for (uint32_t c = blockIdx.x; c < nb; c += gridDim.x)
+    chunk_firsts(a, c, true, cnt, cmask, mism, ctl);
   __builtin_amdgcn_s_waitcnt(0);  // every storing wave drains before the arrival
   __syncthreads();
   if (threadIdx.x == 0) {
-    // arrival: the shard of this chunk, then (its last arriver) the shard count
-    const uint32_t s = c % kShards;
+    // arrival: the workgroup's shard, then (its last arriver) the shard count
+    const uint32_t s = blockIdx.x % kShards, g = gridDim.x;
     bool last = false;
-    if (add_agent(&ctl.shard[s * kLineW], 1u) == shard_size(nb, s) - 1u) {
-      const uint32_t used = nb < kShards ? nb : kShards;
+    if (add_agent(&ctl.shard[s * kShardW], 1u) == shard_size(g, s) - 1u) {
+      const uint32_t used = g < kShards ? g : kShards;
       last = add_agent(&ctl.top[0], 1u) == used - 1u;
     }
     s_last = last;
@@ -1403,14 +1364,11 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   tail_scan(a, nb, cnt, cbase, ctl, s_part);
 }
 
-__global__ __launch_bounds__(kBlock) void nat64_tail_patch(Nat64Args a, uint32_t nb) {
-  if (a.pm.state[4u + a.par] == 0u) return;  // nothing deferred: no new key
-  const uint32_t *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
-  const TailCtl ctl = tail_ctl(a);
-  const uint32_t port_base = ctl.top[2];
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
-  if (ps == kNoSlot || !(ps & (kLocalBit | kPatchBit))) return;
+// One deferred packet: its key's port, the commit of a first packet, and
+// the frame's port and checksum.
+__device__ __forceinline__ void patch_packet(const Nat64Args &a, uint32_t i, uint32_t ps,
+                                             uint32_t port_base, const uint32_t *cbase,
+                                             const uint32_t *cmask) {
   uint32_t *w = a.pm.slots[ps & kSlotMask].w;
   uint32_t port;
   if (ps & kLocalBit) {
@@ -1447,21 +1405,30 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_patch(Nat64Args a, uint32_t
   } else {  // (repair) a committed key found for a colliding packet
     port = w[6] >> 16;
   }
-  // The frame was written with source port 0 and the checksum c0 of that
-  // frame; set the port and patch the checksum, ~fold(~c0 + port) -- exact:
-  // the sum behind c0 includes the pseudo-header's protocol 6, so it is
-  // never 0 and ~c0 recovers its fold.
-  uint8_t *o = a.out_arena + a.out_off[i];
-  // the VLAN depth from the output's Ethernet header (the input's own)
-  const uint32_t marker = ((uint32_t)o[12] << 8) | o[13];
-  const uint32_t k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
-  uint8_t *tcp = o + 34u + 4u * k;  // the TCP header
-  const uint32_t c0 = ((uint32_t)tcp[16] << 8) | tcp[17];
+  // The fused kernel wrote the frame with source port 0 and stashed that
+  // frame's checksum c0 and VLAN depth; set the port and patch the checksum,
+  // ~fold(~c0 + port) -- exact: the sum behind c0 includes the
+  // pseudo-header's protocol 6, so it is never 0 and ~c0 recovers its fold
+  // (DESIGN.md §3.3).  Only the 4 bytes are touched: the frame is not read.
+  const uint32_t ck = a.stash_c0[i];
+  const uint32_t c0 = ck & 0xffffu, k = ck >> 16;
   const uint32_t c = (~fold32(((~c0) & 0xffffu) + port)) & 0xffffu;
+  uint8_t *tcp = a.out_arena + a.out_off[i] + 34u + 4u * k;  // the TCP header
   tcp[0] = (uint8_t)(port >> 8);
   tcp[1] = (uint8_t)port;
   tcp[16] = (uint8_t)(c >> 8);
   tcp[17] = (uint8_t)c;
+}
+
+__global__ __launch_bounds__(kBlock) void nat64_tail_patch(Nat64Args a, uint32_t nb) {
+  if (a.pm.state[4u + a.par] == 0u) return;  // nothing deferred: no new key
+  const uint32_t *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
+  const uint32_t port_base = tail_ctl(a).top[2];
+  for (uint32_t c = blockIdx.x; c < nb; c += gridDim.x) {
+    const uint32_t i = c * kBlock + threadIdx.x;
+    const uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
+    if (ps != kNoSlot && (ps & (kLocalBit | kPatchBit))) patch_packet(a, i, ps, port_base, cbase, cmask);
+  }
 }
 
 // ============================ 4to6 direction =================================
@@ -1775,6 +1742,7 @@ __device__ __forceinline__ void quad_4to6(const Nat64Args &a, rsrc_t rs, rsrc_t 
   f.new_len = d.nl;
   ipv6_header(v, d.nl, s0, f.V, f.ph);
   f.info = v.k | kNow | ((rport & 0xffffu) << 16);  // the original v6-side port
+  f.defer_i = kNoSlot;
   rewrite_quad<false>(a, rs, ors, g, d, al16, f, X, E);
 }
 
@@ -1817,10 +1785,10 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
 }  // namespace
 
 uint32_t nat64_num_blocks(uint32_t n) { return (n + kBlock - 1) / kBlock; }
-size_t nat64_ctl_offset(uint32_t n) {
-  return 4ull * (10ull * nat64_num_blocks(n) + ((n + kLineW - 1u) / kLineW) * kLineW);
+size_t nat64_ctl_offset(uint32_t n) {  // 4 KiB aligned within the scratch's chunk area
+  return (4ull * (10ull * nat64_num_blocks(n) + n) + 4095ull) & ~4095ull;
 }
-size_t nat64_chunk_bytes(uint32_t n) { return nat64_ctl_offset(n) + 4ull * (kShards + 1u) * kLineW; }
+size_t nat64_chunk_bytes(uint32_t n) { return nat64_ctl_offset(n) + 4ull * (kShards * kShardW + 32u); }
 
 hipError_t launch_portmap_init(const PortMapDev &pm, uint32_t first_port, hipStream_t s) {
   // one thread per slot and ADDR_MAP entry
@@ -1840,8 +1808,9 @@ hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s, hipEvent_t done)
   hipLaunchKernelGGL(nat64_6to4_fused, dim3(nbf), dim3(kBlock), 0, s, a);
   // the tail: the order of the new keys, then their frames' ports; in the
   // steady state (no new key) both grids return at once
-  hipLaunchKernelGGL(nat64_tail_order, dim3(nb), dim3(kBlock), 0, s, a, nb);
-  hipExtLaunchKernelGGL(nat64_tail_patch, dim3(nb), dim3(kBlock), 0, s, nullptr, done, 0, a, nb);
+  hipLaunchKernelGGL(nat64_tail_order, dim3(nb < kOrderGrid ? nb : kOrderGrid), dim3(kBlock), 0, s, a, nb);
+  hipExtLaunchKernelGGL(nat64_tail_patch, dim3(nb < kPatchGrid ? nb : kPatchGrid), dim3(kBlock), 0, s,
+                        nullptr, done, 0, a, nb);
   return hipGetLastError();
 }
 
