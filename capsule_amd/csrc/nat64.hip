@@ -1100,8 +1100,9 @@ __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a
 //                        first packet also commits the key (port, kPersist,
 //                        ADDR_MAP).
 // Both are grid-stride loops over the chunks on grids of at most kOrderGrid
-// / kPatchGrid workgroups: in the steady state each workgroup only reads
-// the flag and returns, so the grid's size is the launch's cost.  Inside
+// / kPatchGrid workgroups (in the steady state each workgroup only reads the
+// flag and returns: 1.5-1.9 us per launch on the stream, nearly independent
+// of the grid up to 1024 workgroups, tools/launch_gap.hip).  Inside
 // nat64_tail_order, the counts and the collision list are stored sc1,
 // drained before the arrival atomics and loaded sc1 by the last workgroup
 // (MI355X_MICROARCH.md, inter-workgroup visibility: the last arriver, told
@@ -1128,7 +1129,7 @@ __device__ __forceinline__ uint32_t add_agent(uint32_t *p, uint32_t v) {
 // then a line with the shard-completion counter, the collision count and
 // the port base.
 constexpr uint32_t kShards = 8u, kShardW = 1024u;
-constexpr uint32_t kOrderGrid = 256u, kPatchGrid = 1024u;
+constexpr uint32_t kOrderGrid = 1024u, kPatchGrid = 4096u;
 struct TailCtl {
   uint32_t *shard;  // [kShards * kShardW]: shard s counts at shard[s * kShardW]
   uint32_t *top;    // [0] shards complete, [1] collisions, [2] port base
@@ -1176,6 +1177,64 @@ __device__ __forceinline__ void chunk_firsts(const Nat64Args &a, uint32_t c, boo
   }
   const uint32_t n_first = (uint32_t)__syncthreads_count(f);
   if (threadIdx.x == 0) st_sc1(&cnt[c], n_first);
+}
+
+// kOrderU chunks per workgroup (c0 + j * stride): every load of the U chunks
+// is issued before the first compare, so a workgroup waits on one chain of
+// dependent loads (pkt_slot -> slot) instead of U; the counts per wave go
+// through LDS (s_wc), one barrier for the U chunks.
+constexpr uint32_t kOrderU = 4u;
+__device__ __forceinline__ void chunks_firsts(const Nat64Args &a, uint32_t c0, uint32_t stride,
+                                              uint32_t nb, uint32_t *cnt, uint32_t *cmask,
+                                              uint32_t *mism, const TailCtl &ctl,
+                                              uint32_t (*s_wc)[kBlock / 64]) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t ps[kOrderU], w7[kOrderU];
+  bool bad[kOrderU];
+#pragma unroll
+  for (uint32_t j = 0; j < kOrderU; ++j) {
+    const uint32_t c = c0 + j * stride, i = c * kBlock + threadIdx.x;
+    ps[j] = c < nb && i < a.n ? a.pkt_slot[i] : kNoSlot;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kOrderU; ++j) {
+    const uint32_t i = (c0 + j * stride) * kBlock + threadIdx.x;
+    w7[j] = kNoSlot;
+    bad[j] = false;
+    if (ps[j] != kNoSlot && (ps[j] & kLocalBit)) {
+      const uint32_t *w = a.pm.slots[ps[j] & kSlotMask].w;
+      w7[j] = w[7];
+      if (!(ps[j] & kClaimBit)) bad[j] = !stash_matches(a, i, w);
+    }
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kOrderU; ++j) {
+    const uint32_t c = c0 + j * stride, i = c * kBlock + threadIdx.x;
+    const bool f = !bad[j] && w7[j] == i;
+    const uint64_t m = __ballot(f);
+    if (lane == 0 && c < nb) {
+      st_sc1(&cmask[8u * c + 2u * wave], (uint32_t)m);
+      st_sc1(&cmask[8u * c + 2u * wave + 1u], (uint32_t)(m >> 32));
+      s_wc[j][wave] = (uint32_t)__popcll(m);
+    }
+    const uint64_t bm = __ballot(bad[j]);
+    if (bm) {  // rare: list the wave's collisions
+      const uint32_t first = (uint32_t)__builtin_ctzll(bm);
+      uint32_t at = 0;
+      if (lane == first) at = add_agent(&ctl.top[1], (uint32_t)__popcll(bm));
+      at = __shfl(at, (int)first);
+      if (bad[j]) st_sc1(&mism[at + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))], i);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kOrderU) {
+    const uint32_t c = c0 + threadIdx.x * stride;
+    uint32_t t = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kBlock / 64u; ++w) t += s_wc[threadIdx.x][w];
+    if (c < nb) st_sc1(&cnt[c], t);
+  }
+  __syncthreads();  // s_wc is reused
 }
 
 // The repair of tag collisions (rare: distinct keys whose claim tags are
@@ -1300,19 +1359,23 @@ __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const
   const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
   uint32_t sum = 0;
   for (uint32_t b = b0; b < b1; ++b) sum += ld_sc1(&cnt[b]);
-  s_part[threadIdx.x] = sum;
-  __syncthreads();
-  if (threadIdx.x == 0) {  // 256 partial sums: one thread
-    uint32_t run = 0;
-    for (uint32_t t = 0; t < kBlock; ++t) {
-      const uint32_t x = s_part[t];
-      s_part[t] = run;
-      run += x;
-    }
-    s_part[kBlock] = run;
+  // exclusive scan of the 256 partial sums: within each wave by shuffles,
+  // then the four wave totals
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t incl = sum;
+#pragma unroll
+  for (uint32_t d = 1; d < 64u; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d);
+    if (lane >= d) incl += y;
   }
+  if (lane == 63u) s_part[wave] = incl;
   __syncthreads();
-  uint32_t run = s_part[threadIdx.x];
+  uint32_t run = incl - sum, total = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kBlock / 64u; ++w) {
+    if (w < wave) run += s_part[w];
+    total += s_part[w];
+  }
   for (uint32_t b = b0; b < b1; ++b) {
     const uint32_t c = ld_sc1(&cnt[b]);
     cbase[b] = run;
@@ -1320,7 +1383,7 @@ __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const
   }
   if (threadIdx.x < kShards) ctl.shard[threadIdx.x * kShardW] = 0u;
   if (threadIdx.x == 0) {
-    const uint32_t total = s_part[kBlock], base = st[0];
+    const uint32_t base = st[0];
     ctl.top[0] = 0u;
     ctl.top[1] = 0u;
     ctl.top[2] = base;
@@ -1335,15 +1398,16 @@ __device__ __forceinline__ uint32_t shard_size(uint32_t grid, uint32_t s) {
 
 __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t nb) {
   __shared__ uint32_t s_last, s_nm;
-  __shared__ uint32_t s_part[kBlock + 1];
+  __shared__ uint32_t s_part[kBlock / 64];
+  __shared__ uint32_t s_wc[kOrderU][kBlock / 64];
   uint32_t *const st = a.pm.state;
   if (blockIdx.x == 0 && threadIdx.x == 0) st[4u + (a.par ^ 1u)] = 0u;  // the previous call's flag
   if (st[4u + a.par] == 0u) return;  // nothing deferred: no new key
   uint32_t *const cnt = a.chunks, *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
   uint32_t *const mism = a.chunks + 10u * nb;  // the tag collisions (packet indices)
   const TailCtl ctl = tail_ctl(a);
-  for (uint32_t c = blockIdx.x; c < nb; c += gridDim.x)
-    chunk_firsts(a, c, true, cnt, cmask, mism, ctl);
+  for (uint32_t c0 = blockIdx.x; c0 < nb; c0 += kOrderU * gridDim.x)
+    chunks_firsts(a, c0, gridDim.x, nb, cnt, cmask, mism, ctl, s_wc);
   __builtin_amdgcn_s_waitcnt(0);  // every storing wave drains before the arrival
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1367,7 +1431,7 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
 // One deferred packet: its key's port, the commit of a first packet, and
 // the frame's port and checksum.
 __device__ __forceinline__ void patch_packet(const Nat64Args &a, uint32_t i, uint32_t ps,
-                                             uint32_t port_base, const uint32_t *cbase,
+                                             uint32_t o_off, uint32_t ck, uint32_t port_base, const uint32_t *cbase,
                                              const uint32_t *cmask) {
   uint32_t *w = a.pm.slots[ps & kSlotMask].w;
   uint32_t port;
@@ -1410,10 +1474,9 @@ __device__ __forceinline__ void patch_packet(const Nat64Args &a, uint32_t i, uin
   // ~fold(~c0 + port) -- exact: the sum behind c0 includes the
   // pseudo-header's protocol 6, so it is never 0 and ~c0 recovers its fold
   // (DESIGN.md §3.3).  Only the 4 bytes are touched: the frame is not read.
-  const uint32_t ck = a.stash_c0[i];
   const uint32_t c0 = ck & 0xffffu, k = ck >> 16;
   const uint32_t c = (~fold32(((~c0) & 0xffffu) + port)) & 0xffffu;
-  uint8_t *tcp = a.out_arena + a.out_off[i] + 34u + 4u * k;  // the TCP header
+  uint8_t *tcp = a.out_arena + o_off + 34u + 4u * k;  // the TCP header
   tcp[0] = (uint8_t)(port >> 8);
   tcp[1] = (uint8_t)port;
   tcp[16] = (uint8_t)(c >> 8);
@@ -1426,8 +1489,10 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_patch(Nat64Args a, uint32_t
   const uint32_t port_base = tail_ctl(a).top[2];
   for (uint32_t c = blockIdx.x; c < nb; c += gridDim.x) {
     const uint32_t i = c * kBlock + threadIdx.x;
-    const uint32_t ps = i < a.n ? a.pkt_slot[i] : kNoSlot;
-    if (ps != kNoSlot && (ps & (kLocalBit | kPatchBit))) patch_packet(a, i, ps, port_base, cbase, cmask);
+    if (i >= a.n) break;
+    // loaded together: the slot reference, the frame's place and its stash
+    const uint32_t ps = a.pkt_slot[i], o_off = a.out_off[i], ck = a.stash_c0[i];
+    if (ps != kNoSlot && (ps & (kLocalBit | kPatchBit))) patch_packet(a, i, ps, o_off, ck, port_base, cbase, cmask);
   }
 }
 
@@ -1805,10 +1870,15 @@ hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s, hipEvent_t done)
   const uint32_t nb = nat64_num_blocks(a.n);
   const uint32_t fpb = (kBlock / 64u) * kRowFrames;  // fused: kRowFrames frames per wave
   const uint32_t nbf = (a.n + fpb - 1) / fpb;
+#ifdef CGPU_NAT64_ABL_NOTAIL  // timing ablation only (steady state): what the tail launches cost
+  hipExtLaunchKernelGGL(nat64_6to4_fused, dim3(nbf), dim3(kBlock), 0, s, nullptr, done, 0, a);
+  return hipGetLastError();
+#endif
   hipLaunchKernelGGL(nat64_6to4_fused, dim3(nbf), dim3(kBlock), 0, s, a);
   // the tail: the order of the new keys, then their frames' ports; in the
   // steady state (no new key) both grids return at once
-  hipLaunchKernelGGL(nat64_tail_order, dim3(nb < kOrderGrid ? nb : kOrderGrid), dim3(kBlock), 0, s, a, nb);
+  const uint32_t og = (nb + kOrderU - 1u) / kOrderU;
+  hipLaunchKernelGGL(nat64_tail_order, dim3(og < kOrderGrid ? og : kOrderGrid), dim3(kBlock), 0, s, a, nb);
   hipExtLaunchKernelGGL(nat64_tail_patch, dim3(nb < kPatchGrid ? nb : kPatchGrid), dim3(kBlock), 0, s,
                         nullptr, done, 0, a, nb);
   return hipGetLastError();
