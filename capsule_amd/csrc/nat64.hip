@@ -1406,8 +1406,15 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   uint32_t *const cnt = a.chunks, *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
   uint32_t *const mism = a.chunks + 10u * nb;  // the tag collisions (packet indices)
   const TailCtl ctl = tail_ctl(a);
+#ifdef CGPU_NAT64_TAIL_CLOCK  // diagnosis only: the order launch's phases, printed for a few calls
+  unsigned long long *clk = reinterpret_cast<unsigned long long *>(ctl.top + 16);
+  if (threadIdx.x == 0) atomicMin(&clk[0], (unsigned long long)wall_clock64());
+#endif
   for (uint32_t c0 = blockIdx.x; c0 < nb; c0 += kOrderU * gridDim.x)
     chunks_firsts(a, c0, gridDim.x, nb, cnt, cmask, mism, ctl, s_wc);
+#ifdef CGPU_NAT64_TAIL_CLOCK
+  if (threadIdx.x == 0) atomicMax(&clk[1], (unsigned long long)wall_clock64());
+#endif
   __builtin_amdgcn_s_waitcnt(0);  // every storing wave drains before the arrival
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1424,8 +1431,24 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   if (!s_last) return;
   if (threadIdx.x == 0) s_nm = atomicCAS(&ctl.top[1], 0u, 0u);  // the collisions, read at the coherence point
   __syncthreads();
+#ifdef CGPU_NAT64_TAIL_CLOCK
+  const unsigned long long t2 = wall_clock64();
+#endif
   if (s_nm) tail_repair(a, nb, s_nm, mism, cnt, cmask, ctl);
   tail_scan(a, nb, cnt, cbase, ctl, s_part);
+#ifdef CGPU_NAT64_TAIL_CLOCK
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t3 = wall_clock64();
+    const unsigned long long t0 = atomicCAS(&clk[0], 0ull, 0ull), t1 = atomicCAS(&clk[1], 0ull, 0ull);
+    const uint32_t call = atomicAdd(ctl.top + 20, 1u);
+    if (call % 256u == 100u)
+      printf("order clock (10 ns): chunks %llu, last chunk -> last arriver %llu, scan %llu, grid %u\n",
+             t1 - t0, t2 - t1, t3 - t2, gridDim.x);
+    atomicExch(&clk[0], ~0ull);
+    atomicExch(&clk[1], 0ull);
+  }
+#endif
 }
 
 // One deferred packet: its key's port, the commit of a first packet, and
@@ -1477,10 +1500,14 @@ __device__ __forceinline__ void patch_packet(const Nat64Args &a, uint32_t i, uin
   const uint32_t c0 = ck & 0xffffu, k = ck >> 16;
   const uint32_t c = (~fold32(((~c0) & 0xffffu) + port)) & 0xffffu;
   uint8_t *tcp = a.out_arena + o_off + 34u + 4u * k;  // the TCP header
+#ifdef CGPU_NAT64_ABL_NOPATCHSTORE  // timing ablation only: the frames are not patched
+  if (c == 0x12345u) tcp[0] = 0;
+#else
   tcp[0] = (uint8_t)(port >> 8);
   tcp[1] = (uint8_t)port;
   tcp[16] = (uint8_t)(c >> 8);
   tcp[17] = (uint8_t)c;
+#endif
 }
 
 __global__ __launch_bounds__(kBlock) void nat64_tail_patch(Nat64Args a, uint32_t nb) {
