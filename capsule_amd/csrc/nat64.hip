@@ -1183,7 +1183,10 @@ __device__ __forceinline__ void chunk_firsts(const Nat64Args &a, uint32_t c, boo
 // is issued before the first compare, so a workgroup waits on one chain of
 // dependent loads (pkt_slot -> slot) instead of U; the counts per wave go
 // through LDS (s_wc), one barrier for the U chunks.
-constexpr uint32_t kOrderU = 4u;
+#ifndef CGPU_NAT64_ORDER_U
+#define CGPU_NAT64_ORDER_U 4
+#endif
+constexpr uint32_t kOrderU = CGPU_NAT64_ORDER_U;
 __device__ __forceinline__ void chunks_firsts(const Nat64Args &a, uint32_t c0, uint32_t stride,
                                               uint32_t nb, uint32_t *cnt, uint32_t *cmask,
                                               uint32_t *mism, const TailCtl &ctl,
@@ -1204,7 +1207,9 @@ __device__ __forceinline__ void chunks_firsts(const Nat64Args &a, uint32_t c0, u
     if (ps[j] != kNoSlot && (ps[j] & kLocalBit)) {
       const uint32_t *w = a.pm.slots[ps[j] & kSlotMask].w;
       w7[j] = w[7];
+#ifndef CGPU_NAT64_ABL_NOVERIFY  // timing ablation only: tag joins trusted
       if (!(ps[j] & kClaimBit)) bad[j] = !stash_matches(a, i, w);
+#endif
     }
   }
 #pragma unroll
@@ -1408,12 +1413,20 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   const TailCtl ctl = tail_ctl(a);
 #ifdef CGPU_NAT64_TAIL_CLOCK  // diagnosis only: the order launch's phases, printed for a few calls
   unsigned long long *clk = reinterpret_cast<unsigned long long *>(ctl.top + 16);
-  if (threadIdx.x == 0) atomicMin(&clk[0], (unsigned long long)wall_clock64());
+  const unsigned long long ts = wall_clock64();
+  if (threadIdx.x == 0) {
+    atomicMin(&clk[0], ts);
+    atomicMax(&clk[3], ts);
+  }
 #endif
   for (uint32_t c0 = blockIdx.x; c0 < nb; c0 += kOrderU * gridDim.x)
     chunks_firsts(a, c0, gridDim.x, nb, cnt, cmask, mism, ctl, s_wc);
 #ifdef CGPU_NAT64_TAIL_CLOCK
-  if (threadIdx.x == 0) atomicMax(&clk[1], (unsigned long long)wall_clock64());
+  if (threadIdx.x == 0) {
+    const unsigned long long te = wall_clock64();
+    atomicMax(&clk[1], te);
+    atomicMax(&clk[4], te - ts);
+  }
 #endif
   __builtin_amdgcn_s_waitcnt(0);  // every storing wave drains before the arrival
   __syncthreads();
@@ -1441,12 +1454,16 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   if (threadIdx.x == 0) {
     const unsigned long long t3 = wall_clock64();
     const unsigned long long t0 = atomicCAS(&clk[0], 0ull, 0ull), t1 = atomicCAS(&clk[1], 0ull, 0ull);
-    const uint32_t call = atomicAdd(ctl.top + 20, 1u);
+    const unsigned long long t4 = atomicCAS(&clk[3], 0ull, 0ull), t5 = atomicCAS(&clk[4], 0ull, 0ull);
+    const uint32_t call = atomicAdd(ctl.top + 26, 1u);
     if (call % 256u == 100u)
-      printf("order clock (10 ns): chunks %llu, last chunk -> last arriver %llu, scan %llu, grid %u\n",
-             t1 - t0, t2 - t1, t3 - t2, gridDim.x);
+      printf("order clock (10 ns): chunks %llu, last chunk -> last arriver %llu, scan %llu, grid %u, "
+             "latest start %llu, longest workgroup %llu\n",
+             t1 - t0, t2 - t1, t3 - t2, gridDim.x, t4 - t0, t5);
     atomicExch(&clk[0], ~0ull);
     atomicExch(&clk[1], 0ull);
+    atomicExch(&clk[3], 0ull);
+    atomicExch(&clk[4], 0ull);
   }
 #endif
 }
