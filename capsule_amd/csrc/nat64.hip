@@ -1206,7 +1206,11 @@ __device__ __forceinline__ void chunks_firsts(const Nat64Args &a, uint32_t c0, u
     bad[j] = false;
     if (ps[j] != kNoSlot && (ps[j] & kLocalBit)) {
       const uint32_t *w = a.pm.slots[ps[j] & kSlotMask].w;
+#ifdef CGPU_NAT64_ABL_NOSLOT  // timing ablation only: no slot read (wrong first packets)
+      w7[j] = (ps[j] & kClaimBit) ? i : kNoSlot;
+#else
       w7[j] = w[7];
+#endif
 #ifndef CGPU_NAT64_ABL_NOVERIFY  // timing ablation only: tag joins trusted
       if (!(ps[j] & kClaimBit)) bad[j] = !stash_matches(a, i, w);
 #endif
@@ -1218,8 +1222,13 @@ __device__ __forceinline__ void chunks_firsts(const Nat64Args &a, uint32_t c0, u
     const bool f = !bad[j] && w7[j] == i;
     const uint64_t m = __ballot(f);
     if (lane == 0 && c < nb) {
+#ifdef CGPU_NAT64_ABL_PLAINST  // timing ablation only (the last arriver may read stale counts)
+      cmask[8u * c + 2u * wave] = (uint32_t)m;
+      cmask[8u * c + 2u * wave + 1u] = (uint32_t)(m >> 32);
+#else
       st_sc1(&cmask[8u * c + 2u * wave], (uint32_t)m);
       st_sc1(&cmask[8u * c + 2u * wave + 1u], (uint32_t)(m >> 32));
+#endif
       s_wc[j][wave] = (uint32_t)__popcll(m);
     }
     const uint64_t bm = __ballot(bad[j]);
@@ -1237,7 +1246,11 @@ __device__ __forceinline__ void chunks_firsts(const Nat64Args &a, uint32_t c0, u
     uint32_t t = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kBlock / 64u; ++w) t += s_wc[threadIdx.x][w];
+#ifdef CGPU_NAT64_ABL_PLAINST
+    if (c < nb) cnt[c] = t;
+#else
     if (c < nb) st_sc1(&cnt[c], t);
+#endif
   }
   __syncthreads();  // s_wc is reused
 }
@@ -1520,10 +1533,15 @@ __device__ __forceinline__ void patch_packet(const Nat64Args &a, uint32_t i, uin
 #ifdef CGPU_NAT64_ABL_NOPATCHSTORE  // timing ablation only: the frames are not patched
   if (c == 0x12345u) tcp[0] = 0;
 #else
-  tcp[0] = (uint8_t)(port >> 8);
-  tcp[1] = (uint8_t)port;
-  tcp[16] = (uint8_t)(c >> 8);
-  tcp[17] = (uint8_t)c;
+  if (!((o_off + 34u) & 1u)) {  // (packed 6to4 output: even) two 16-bit stores
+    *reinterpret_cast<uint16_t *>(tcp) = (uint16_t)swap16(port);
+    *reinterpret_cast<uint16_t *>(tcp + 16) = (uint16_t)swap16(c);
+  } else {
+    tcp[0] = (uint8_t)(port >> 8);
+    tcp[1] = (uint8_t)port;
+    tcp[16] = (uint8_t)(c >> 8);
+    tcp[17] = (uint8_t)c;
+  }
 #endif
 }
 
