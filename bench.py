@@ -910,6 +910,39 @@ def e2e_mbufs(args):
     ctx.close()
 
 
+def numa_report(dev, tensors):
+    """NUMA placement for the end-to-end rates: the GPU's node (sysfs) and the
+    nodes of a sample of pages of each pinned host tensor (move_pages(2) with
+    no target nodes reports where each page lives).  A pinned buffer on the
+    node away from the GPU's PCIe root crosses the socket link on every DMA."""
+    import ctypes
+    import torch
+
+    out = {}
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            out["gpu_node"] = int(f.read())
+    except (OSError, ValueError, RuntimeError):
+        out["gpu_node"] = None
+    libc = ctypes.CDLL(None, use_errno=True)
+    page = os.sysconf("SC_PAGE_SIZE")
+    for name, t in tensors.items():
+        nb = t.numel() * t.element_size()
+        k = max(1, min(64, nb // page))
+        addrs = (ctypes.c_void_p * k)(*[(t.data_ptr() + (nb * j // k)) & ~(page - 1) for j in range(k)])
+        status = (ctypes.c_int * k)()
+        if libc.syscall(279, 0, ctypes.c_ulong(k), addrs, None, status, 0) != 0:  # SYS_move_pages
+            out[name] = f"move_pages errno {ctypes.get_errno()}"
+            continue
+        hist = {}
+        for v in status:
+            hist[str(v)] = hist.get(str(v), 0) + 1
+        out[name] = hist
+    return out
+
+
 def e2e(args):
     """End-to-end rate with the batch starting and ending in host memory.
 
@@ -1002,7 +1035,8 @@ def e2e(args):
         "steps": steps, "packets_per_step": n, "ms_per_step": round(el / steps * 1e3, 3),
         "h2d_GBps": round(up_bytes * steps / el / 1e9, 2),
         "d2h_GBps": round(down_bytes * steps / el / 1e9, 2),
-        "batches_in_flight": D}), flush=True)
+        "batches_in_flight": D,
+        "numa": numa_report(dev, {"h2d_src": host["arena"], "d2h_dst": host_out[0][0]})}), flush=True)
     ctx.close()
 
 

@@ -12,7 +12,8 @@
 //
 // The reference assigns gateway ports from a global AtomicU16 (first 1025)
 // in first-seen order of (v6 src, tcp src port).  A batch reproduces that
-// order exactly.  6to4 is two launches, 4to6 one.
+// order exactly.  6to4 is three launches (the fused kernel, the tail's order
+// and patch launches), 4to6 one.
 //
 // The fused kernels (nat64_6to4_fused, nat64_4to6_fused): a wave owns 32
 // frames.  Waves whose frames are 16-B aligned in the input, dword-aligned
@@ -28,12 +29,13 @@
 // frame (any alignment, any length), DPP quad broadcasts of the header.
 //
 // A 6to4 frame whose key is not yet committed (first seen in this batch) is
-// written with source port 0 and deferred: its key is claimed or joined in
-// the slot table (claim tags, keys published with atomics: probe_port_at),
-// and the tail kernel (nat64_tail) orders the batch's new keys by their
-// first packet, assigns NEXT_PORT + ordinal, commits them, and patches only
-// the deferred frames' port and checksum.  With no new key (the steady
-// state) the tail returns at once.
+// written with source port 0 and deferred (its checksum stashed): its key is
+// claimed in the slot table or joined on the claim's tag (probe_port_at),
+// and the tail (nat64_tail_order, nat64_tail_patch) verifies the tag joins,
+// orders the batch's new keys by their first packet, assigns NEXT_PORT +
+// ordinal, commits them, and patches only the deferred frames' port and
+// checksum.  With no new key (the steady state) both tail launches return at
+// once.
 #include <hip/hip_ext.h>
 
 #include "capsule_gpu.h"

@@ -88,19 +88,21 @@ int main() {
   hipEvent_t rec_t;
   CK(hipEventCreate(&rec_t));
   const char *names[] = {"ext_launch stop event (no timing flag)", "ext_launch stop event (timing)",
-                         "event_record + wait_event same stream", "wait_event only (old event)"};
-  for (int mode = 0; mode < 4; ++mode) {
+                         "event_record + wait_event same stream", "wait_event only (old event)",
+                         "ext_launch stop event + wait on it next iter"};
+  for (int mode = 0; mode < 5; ++mode) {
     for (int rep = 0; rep < 2; ++rep) {
       CK(hipEventRecord(a, s));
       for (int it = 0; it < iters; ++it) {
-        if (mode == 0)
+        if (mode == 4) CK(hipStreamWaitEvent(s, rec, 0));  // the previous iteration's, not yet complete
+        if (mode == 0 || mode == 4)
           hipExtLaunchKernelGGL(stream, dim3(2048), dim3(256), 0, s, nullptr, rec, 0, buf, bytes / 16, out);
         else if (mode == 1)
           hipExtLaunchKernelGGL(stream, dim3(2048), dim3(256), 0, s, nullptr, rec_t, 0, buf, bytes / 16, out);
         else
           hipLaunchKernelGGL(stream, dim3(2048), dim3(256), 0, s, buf, bytes / 16, out);
         if (mode == 2) CK(hipEventRecord(rec, s));
-        if (mode >= 2) CK(hipStreamWaitEvent(s, rec, 0));
+        if (mode == 2 || mode == 3) CK(hipStreamWaitEvent(s, rec, 0));
       }
       CK(hipEventRecord(b, s));
       CK(hipEventSynchronize(b));
@@ -110,5 +112,27 @@ int main() {
       if (rep == 1) printf("%-42s us/iter=%8.2f  extra=%7.2f\n", names[mode], us, us - base);
     }
   }
+  // stream ids: are they reused after a destroy (the nat64 map's "same
+  // stream as the previous call" test must not be fooled by a new stream
+  // that got an old handle)?
+  unsigned long long prev_id = 0;
+  int handle_reuse = 0, id_reuse = 0;
+  void *prev_h = nullptr;
+  for (int k = 0; k < 64; ++k) {
+    hipStream_t t;
+    CK(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
+    unsigned long long id;
+    CK(hipStreamGetId(t, &id));
+    if ((void *)t == prev_h) ++handle_reuse;
+    if (k && id == prev_id) ++id_reuse;
+    if (k < 4) printf("stream %p id %llu\n", (void *)t, id);
+    prev_h = (void *)t;
+    prev_id = id;
+    CK(hipStreamDestroy(t));
+  }
+  unsigned long long id0;
+  CK(hipStreamGetId(s, &id0));
+  printf("64 create/destroy: handle reused %d times, id reused %d times; bench stream id %llu\n",
+         handle_reuse, id_reuse, id0);
   return 0;
 }
