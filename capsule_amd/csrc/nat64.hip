@@ -1412,6 +1412,11 @@ __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const
   }
 }
 
+#ifdef CGPU_NAT64_TAIL_CLOCK
+__device__ unsigned long long g_clk[2 * kOrderGrid];
+__device__ uint32_t g_clk_calls;
+#endif
+
 __device__ __forceinline__ uint32_t shard_size(uint32_t grid, uint32_t s) {
   return s < grid ? (grid - s + kShards - 1u) / kShards : 0u;
 }
@@ -1427,20 +1432,19 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   uint32_t *const mism = a.chunks + 10u * nb;  // the tag collisions (packet indices)
   const TailCtl ctl = tail_ctl(a);
 #ifdef CGPU_NAT64_TAIL_CLOCK  // diagnosis only: the order launch's phases, printed for a few calls
-  unsigned long long *clk = reinterpret_cast<unsigned long long *>(ctl.top + 16);
+  // per workgroup (start, end of its chunks) in a device array, plain
+  // write-through stores: no atomics of their own
   const unsigned long long ts = wall_clock64();
-  if (threadIdx.x == 0) {
-    atomicMin(&clk[0], ts);
-    atomicMax(&clk[3], ts);
-  }
 #endif
+#ifndef CGPU_NAT64_ABL_NOCHUNKS  // timing ablation only: the arrival and the scan alone
   for (uint32_t c0 = blockIdx.x; c0 < nb; c0 += kOrderU * gridDim.x)
     chunks_firsts(a, c0, gridDim.x, nb, cnt, cmask, mism, ctl, s_wc);
+#endif
 #ifdef CGPU_NAT64_TAIL_CLOCK
   if (threadIdx.x == 0) {
-    const unsigned long long te = wall_clock64();
-    atomicMax(&clk[1], te);
-    atomicMax(&clk[4], te - ts);
+    __hip_atomic_store(&g_clk[2 * blockIdx.x], ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&g_clk[2 * blockIdx.x + 1], (unsigned long long)wall_clock64(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
 #endif
   __builtin_amdgcn_s_waitcnt(0);  // every storing wave drains before the arrival
@@ -1468,17 +1472,21 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned long long t3 = wall_clock64();
-    const unsigned long long t0 = atomicCAS(&clk[0], 0ull, 0ull), t1 = atomicCAS(&clk[1], 0ull, 0ull);
-    const unsigned long long t4 = atomicCAS(&clk[3], 0ull, 0ull), t5 = atomicCAS(&clk[4], 0ull, 0ull);
-    const uint32_t call = atomicAdd(ctl.top + 26, 1u);
+    unsigned long long s0 = ~0ull, s1 = 0, e1 = 0, dmax = 0, dsum = 0;
+    for (uint32_t b = 0; b < gridDim.x; ++b) {
+      const unsigned long long x = __hip_atomic_load(&g_clk[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long y = __hip_atomic_load(&g_clk[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s0 = x < s0 ? x : s0;
+      s1 = x > s1 ? x : s1;
+      e1 = y > e1 ? y : e1;
+      dmax = y - x > dmax ? y - x : dmax;
+      dsum += y - x;
+    }
+    const uint32_t call = g_clk_calls++;
     if (call % 256u == 100u)
-      printf("order clock (10 ns): chunks %llu, last chunk -> last arriver %llu, scan %llu, grid %u, "
-             "latest start %llu, longest workgroup %llu\n",
-             t1 - t0, t2 - t1, t3 - t2, gridDim.x, t4 - t0, t5);
-    atomicExch(&clk[0], ~0ull);
-    atomicExch(&clk[1], 0ull);
-    atomicExch(&clk[3], 0ull);
-    atomicExch(&clk[4], 0ull);
+      printf("order clock (10 ns): first start -> last chunk end %llu, last start %llu, workgroup mean %llu max %llu, "
+             "-> last arriver %llu, scan %llu, grid %u\n",
+             e1 - s0, s1 - s0, dsum / gridDim.x, dmax, t2 - e1, t3 - t2, gridDim.x);
   }
 #endif
 }
@@ -1911,6 +1919,13 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
   }
 }
 
+#ifdef CGPU_NAT64_DIAG_GAP_US
+__global__ void diag_spin(unsigned long long ticks) {  // wall clock: 100 MHz
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+#endif
+
 }  // namespace
 
 uint32_t nat64_num_blocks(uint32_t n) { return (n + kBlock - 1) / kBlock; }
@@ -1939,6 +1954,9 @@ hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s, hipEvent_t done)
   return hipGetLastError();
 #endif
   hipLaunchKernelGGL(nat64_6to4_fused, dim3(nbf), dim3(kBlock), 0, s, a);
+#ifdef CGPU_NAT64_DIAG_GAP_US  // diagnosis only: an idle gap between the fused kernel and the tail
+  hipLaunchKernelGGL(diag_spin, dim3(1), dim3(64), 0, s, (unsigned long long)(CGPU_NAT64_DIAG_GAP_US) * 100ull);
+#endif
   // the tail: the order of the new keys, then their frames' ports; in the
   // steady state (no new key) both grids return at once
   const uint32_t og = (nb + kOrderU - 1u) / kOrderU;

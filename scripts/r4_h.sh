@@ -13,3 +13,4 @@ for c in nat64 nat64_4to6 nat64 nat64_4to6; do
 done
 export AB_STEPS=2000
 step wait_ab 170 bash scripts/ab_variants.sh "nat64 nat64_4to6" "-" new alwayswait
+bash scripts/r4_j.sh
