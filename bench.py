@@ -1001,41 +1001,69 @@ def e2e(args):
     ev_up = [torch.cuda.Event() for _ in range(D)]
     ev_comp = [torch.cuda.Event() for _ in range(D)]
     ev_down = [torch.cuda.Event() for _ in range(D)]
+    # phase clocks of the timed steps (start / end of each stream's part):
+    # how long each copy and the kernel take, and whether they overlap
+    T = 10
+    ph = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(T)]
+    tr = {"k0": None}
+
+    def mark(k, j, s):
+        if tr["k0"] is not None and 0 <= k - tr["k0"] < T:
+            ph[k - tr["k0"]][j].record(s)
 
     def step(k):
         d = k % D
         with torch.cuda.stream(h2d):
             h2d.wait_event(ev_down[d])  # buffer d free again (its results went home)
+            mark(k, 0, h2d)
             bufs[d].arena.copy_(host["arena"], non_blocking=True)
             bufs[d].off.copy_(host["off"], non_blocking=True)
             bufs[d].len.copy_(host["len"], non_blocking=True)
+            mark(k, 1, h2d)
             ev_up[d].record(h2d)
         comp.wait_event(ev_up[d])
+        mark(k, 2, comp)
         launch[d]()
+        mark(k, 3, comp)
         ev_comp[d].record(comp)
         with torch.cuda.stream(d2h):
             d2h.wait_event(ev_comp[d])
+            mark(k, 4, d2h)
             back(d)
+            mark(k, 5, d2h)
             ev_down[d].record(d2h)
 
     for d in range(D):
         ev_down[d].record(d2h)
-    for k in range(max(3, args.warmup // 10)):
+    for t in ph:  # create the timing events' HIP objects before the timed region
+        for e in t:
+            e.record(comp)
+    kw = max(3, args.warmup // 10)
+    for k in range(kw):
         step(k)
     torch.cuda.synchronize(dev)
     steps = max(10, args.steps // 10)
+    tr["k0"] = kw + steps // 2
     t0 = time.perf_counter()
     for k in range(steps):
         step(k)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
+    n_tr = min(T, steps - steps // 2)
+
+    def mean_ms(j0, j1):
+        return round(sum(ph[t][j0].elapsed_time(ph[t][j1]) for t in range(n_tr)) / n_tr, 3)
+
+    phases = {"h2d_ms": mean_ms(0, 1), "kernel_ms": mean_ms(2, 3), "d2h_ms": mean_ms(4, 5),
+              "h2d_start_to_next_ms": round(sum(ph[t][0].elapsed_time(ph[t + 1][0])
+                                                for t in range(n_tr - 1)) / max(1, n_tr - 1), 3)}
     print(json.dumps({
         "metric": "end-to-end Mpps, host-resident batches (pinned H2D + kernel + D2H)",
         "value": round(n * steps / el / 1e6, 2), "unit": "Mpps", "config": args.config,
         "steps": steps, "packets_per_step": n, "ms_per_step": round(el / steps * 1e3, 3),
         "h2d_GBps": round(up_bytes * steps / el / 1e9, 2),
         "d2h_GBps": round(down_bytes * steps / el / 1e9, 2),
-        "batches_in_flight": D,
+        "batches_in_flight": D, "phases": phases,
         "numa": numa_report(dev, {"h2d_src": host["arena"], "d2h_dst": host_out[0][0]})}), flush=True)
     ctx.close()
 

@@ -1207,14 +1207,22 @@ __device__ __forceinline__ void chunks_firsts(const Nat64Args &a, uint32_t c0, u
     w7[j] = kNoSlot;
     bad[j] = false;
     if (ps[j] != kNoSlot && (ps[j] & kLocalBit)) {
-      const uint32_t *w = a.pm.slots[ps[j] & kSlotMask].w;
+      // the slot in two 16-B loads (w[2..7]: key words and first packet):
+      // a gather costs per instruction and per line, not per byte
+      const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[ps[j] & kSlotMask]);
 #ifdef CGPU_NAT64_ABL_NOSLOT  // timing ablation only: no slot read (wrong first packets)
       w7[j] = (ps[j] & kClaimBit) ? i : kNoSlot;
 #else
-      w7[j] = w[7];
-#endif
+      const u32x4 s1 = sp[1];
+      w7[j] = s1[3];
 #ifndef CGPU_NAT64_ABL_NOVERIFY  // timing ablation only: tag joins trusted
-      if (!(ps[j] & kClaimBit)) bad[j] = !stash_matches(a, i, w);
+      if (!(ps[j] & kClaimBit)) {
+        const u32x4 s0 = sp[0];
+        const u32x4 k = a.stash_key[i];
+        bad[j] = k[0] != s0[2] || k[1] != s0[3] || k[2] != s1[0] || k[3] != s1[1] ||
+                 (uint32_t)a.stash_port[i] != (s1[2] & 0xffffu);
+      }
+#endif
 #endif
     }
   }
@@ -1377,8 +1385,27 @@ __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const
   uint32_t *const st = a.pm.state;
   const uint32_t per = (nb + kBlock - 1u) / kBlock;
   const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
+  // Up to 16 counts per thread (1 Mi packets) are read at once, 16 B per
+  // sc1 load (aux 16), and kept in registers for the second pass: atomic
+  // loads one after the other were a round trip each, 6.8 us.
+  constexpr uint32_t kReg = 16;
+  uint32_t v[kReg];
   uint32_t sum = 0;
-  for (uint32_t b = b0; b < b1; ++b) sum += ld_sc1(&cnt[b]);
+  const bool reg = per <= kReg;
+  if (reg) {
+    const rsrc_t rc = make_rsrc(cnt, 4u * nb);  // counts past nb read as 0
+#pragma unroll
+    for (uint32_t q = 0; q < kReg / 4u; ++q) {
+      const u32x4 t = 4u * q < per ? __builtin_amdgcn_raw_buffer_load_b128(rc, (int)(4u * (b0 + 4u * q)), 0, 16)
+                                   : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) v[4u * q + j] = 4u * q + j < per && b0 + 4u * q + j < nb ? t[j] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kReg; ++j) sum += v[j];
+  } else {
+    for (uint32_t b = b0; b < b1; ++b) sum += ld_sc1(&cnt[b]);
+  }
   // exclusive scan of the 256 partial sums: within each wave by shuffles,
   // then the four wave totals
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -1396,10 +1423,18 @@ __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const
     if (w < wave) run += s_part[w];
     total += s_part[w];
   }
-  for (uint32_t b = b0; b < b1; ++b) {
-    const uint32_t c = ld_sc1(&cnt[b]);
-    cbase[b] = run;
-    run += c;
+  if (reg) {
+#pragma unroll
+    for (uint32_t j = 0; j < kReg; ++j) {
+      if (b0 + j < b1) cbase[b0 + j] = run;
+      run += v[j];
+    }
+  } else {
+    for (uint32_t b = b0; b < b1; ++b) {
+      const uint32_t c = ld_sc1(&cnt[b]);
+      cbase[b] = run;
+      run += c;
+    }
   }
   if (threadIdx.x < kShards) ctl.shard[threadIdx.x * kShardW] = 0u;
   if (threadIdx.x == 0) {

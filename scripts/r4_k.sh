@@ -9,3 +9,6 @@ for v in clock clock_nov clock_noslot; do
 done
 export CFG=nat64_cold
 step cold_nochunks 170 bash scripts/ab_stats.sh nochunks
+for c in nat64 nat64_4to6; do
+  step e2e_$c 170 python bench.py --e2e --config $c --steps 300 --warmup 50
+done
