@@ -960,6 +960,12 @@ def e2e(args):
         raise SystemExit("--e2e: nat64_cold is a device-resident timing of the map's first pass")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    # the pipeline's streams first, before the library's context stream and
+    # any setup work (the order in which streams are created and first used
+    # decides which of them share a hardware queue)
+    h2d, comp, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    if os.environ.get("CGPU_E2E_STREAMS_LATE") == "1":  # the round-3 order (A/B only)
+        h2d = comp = d2h = None
     w = make_workload(args.config, 0xC0FFEE + 2, n=args.n)
     n = len(w["off"])
     ctx = packets.Context(0)
@@ -971,7 +977,8 @@ def e2e(args):
     bufs = [packets.PacketBatch(torch.empty_like(host["arena"], device=dev),
                                 torch.empty_like(host["off"], device=dev),
                                 torch.empty_like(host["len"], device=dev)) for _ in range(D)]
-    h2d, comp, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    if h2d is None:
+        h2d, comp, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     if w["kind"] == "parse":
         outs = [packets.ParseBuffers(n, dev, csum=False) for _ in range(D)]
         host_out = [(torch.empty(n, dtype=torch.int32, pin_memory=True),
