@@ -963,7 +963,14 @@ def e2e(args):
     # the pipeline's streams first, before the library's context stream and
     # any setup work (the order in which streams are created and first used
     # decides which of them share a hardware queue)
-    h2d, comp, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    # Two streams: the upload and the kernel share one (the kernel is 1-2 % of
+    # a batch's upload), the download has its own.  With three, the box's 4
+    # hardware queues (GPU_MAX_HW_QUEUES, HIP's default) could put two of
+    # the pipeline's streams on one queue: 4to6 then ran its uploads and
+    # downloads one after the other, 107 against 182 Mpps.
+    nstreams = int(os.environ.get("CGPU_E2E_STREAMS", "2"))
+    h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    comp = h2d if nstreams == 2 else torch.cuda.Stream(dev)
     if os.environ.get("CGPU_E2E_STREAMS_LATE") == "1":  # the round-3 order (A/B only)
         h2d = comp = d2h = None
     w = make_workload(args.config, 0xC0FFEE + 2, n=args.n)
@@ -978,7 +985,8 @@ def e2e(args):
                                 torch.empty_like(host["off"], device=dev),
                                 torch.empty_like(host["len"], device=dev)) for _ in range(D)]
     if h2d is None:
-        h2d, comp, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        comp = h2d if nstreams == 2 else torch.cuda.Stream(dev)
     if w["kind"] == "parse":
         outs = [packets.ParseBuffers(n, dev, csum=False) for _ in range(D)]
         host_out = [(torch.empty(n, dtype=torch.int32, pin_memory=True),
@@ -1070,7 +1078,7 @@ def e2e(args):
         "steps": steps, "packets_per_step": n, "ms_per_step": round(el / steps * 1e3, 3),
         "h2d_GBps": round(up_bytes * steps / el / 1e9, 2),
         "d2h_GBps": round(down_bytes * steps / el / 1e9, 2),
-        "batches_in_flight": D, "phases": phases,
+        "batches_in_flight": D, "streams": nstreams, "phases": phases,
         "numa": numa_report(dev, {"h2d_src": host["arena"], "d2h_dst": host_out[0][0]})}), flush=True)
     ctx.close()
 
