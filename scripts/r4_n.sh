@@ -6,3 +6,4 @@ for c in nat64_4to6 nat64 parse64 imix_csum; do
   step e2e3_$c 170 env CGPU_E2E_STREAMS=3 python bench.py --e2e --config $c --steps 300 --warmup 50
 done
 grep -h '^{' gpurun_out/e2e[23]_*.log
+step launch_gap 120 tools/launch_gap

@@ -34,6 +34,35 @@ __global__ __launch_bounds__(256) void stream(const u32x4 *p, size_t n16, uint32
   if (acc == 0x9e3779b9u) out[blockIdx.x] = acc;
 }
 
+// The same streams with the first and last wall-clock reading of each
+// workgroup (100 MHz): the kernel's active span, to set against its share of
+// the stream's timeline.
+__global__ __launch_bounds__(256) void stream_clk(const u32x4 *p, size_t n16, uint32_t *out,
+                                                  unsigned long long *clk) {
+  const unsigned long long t0 = wall_clock64();
+  uint32_t acc = 0;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256ull) {
+    u32x4 v = p[i];
+    acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+  }
+  if (acc == 0x9e3779b9u) out[blockIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    clk[2 * blockIdx.x] = t0;
+    clk[2 * blockIdx.x + 1] = wall_clock64();
+  }
+}
+__global__ __launch_bounds__(256) void write_clk(u32x4 *p, size_t n16, unsigned long long *clk) {
+  const unsigned long long t0 = wall_clock64();
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256ull)
+    p[i] = u32x4{(uint32_t)i, 1u, 2u, 3u};
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    clk[2 * blockIdx.x] = t0;
+    clk[2 * blockIdx.x + 1] = wall_clock64();
+  }
+}
+
 __global__ __launch_bounds__(256) void empty(const uint32_t *flag, uint32_t *out) {
   if (*flag == 0u) return;  // the steady state: nothing deferred
   out[blockIdx.x * 256 + threadIdx.x] = 1u;
@@ -111,6 +140,36 @@ int main() {
       const double us = ms * 1e3 / iters;
       if (rep == 1) printf("%-42s us/iter=%8.2f  extra=%7.2f\n", names[mode], us, us - base);
     }
+  }
+  // a kernel's active span against its share of the stream (back to back):
+  // reads only, and writes (whose dirty L2 lines the end-of-kernel release
+  // writes back)
+  {
+    unsigned long long *clk, hclk[2 * 2048];
+    CK(hipMalloc(&clk, sizeof(hclk)));
+    for (int wr = 0; wr < 2; ++wr) {
+      for (int rep = 0; rep < 2; ++rep) {
+        CK(hipEventRecord(a, s));
+        for (int it = 0; it < iters; ++it) {
+          if (wr) hipLaunchKernelGGL(write_clk, dim3(2048), dim3(256), 0, s, buf, bytes / 16, clk);
+          else hipLaunchKernelGGL(stream_clk, dim3(2048), dim3(256), 0, s, buf, bytes / 16, out, clk);
+        }
+        CK(hipEventRecord(b, s));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        CK(hipMemcpy(hclk, clk, sizeof(hclk), hipMemcpyDeviceToHost));
+        unsigned long long lo = ~0ull, hi = 0;
+        for (int k = 0; k < 2048; ++k) {
+          lo = hclk[2 * k] < lo ? hclk[2 * k] : lo;
+          hi = hclk[2 * k + 1] > hi ? hclk[2 * k + 1] : hi;
+        }
+        if (rep == 1)
+          printf("%s 256 MiB: %.2f us per launch on the stream, last launch's workgroups active %.2f us\n",
+                 wr ? "write" : "read ", ms * 1e3 / iters, (hi - lo) / 100.0);
+      }
+    }
+    CK(hipFree(clk));
   }
   // stream ids: are they reused after a destroy (the nat64 map's "same
   // stream as the previous call" test must not be fooled by a new stream
