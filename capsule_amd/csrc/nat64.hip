@@ -1287,6 +1287,7 @@ __device__ void tail_repair(const Nat64Args &a, uint32_t nb, uint32_t nmism, con
   // 1. the listed packets, one by one (thread 0): exact lookups
   if (threadIdx.x == 0) {
     auto add_chunk = [&](uint32_t pkt) {
+      if (pkt >= a.n) return;  // (no packet: nothing to count again)
       const uint32_t ch = pkt / kBlock;
       for (uint32_t q = 0; q < s_nc; ++q)
         if (s_chunk[q] == ch) return;
@@ -1364,7 +1365,7 @@ __device__ void tail_repair(const Nat64Args &a, uint32_t nb, uint32_t nmism, con
       const uint32_t ch = s_min[k] / kBlock;
       bool have = false;
       for (uint32_t q = 0; q < s_nc; ++q) have |= s_chunk[q] == ch;
-      if (!have) {
+      if (!have && s_min[k] < a.n) {
         if (s_nc < 4u * kRepairSet) s_chunk[s_nc++] = ch;
         else s_all = 1u;
       }
@@ -1372,7 +1373,10 @@ __device__ void tail_repair(const Nat64Args &a, uint32_t nb, uint32_t nmism, con
   __syncthreads();
   // 3. count the affected chunks again (every chunk when the sets overflowed)
   const uint32_t nc = s_all ? nb : s_nc;
-  for (uint32_t q = 0; q < nc; ++q) chunk_firsts(a, s_all ? q : s_chunk[q], false, cnt, cmask, nullptr, ctl);
+  for (uint32_t q = 0; q < nc; ++q) {
+    const uint32_t c = s_all ? q : s_chunk[q];  // < nb (add_chunk keeps packets < n)
+    chunk_firsts(a, c, false, cnt, cmask, nullptr, ctl);
+  }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
 }
@@ -1574,6 +1578,10 @@ __device__ __forceinline__ void patch_packet(const Nat64Args &a, uint32_t i, uin
   // (DESIGN.md §3.3).  Only the 4 bytes are touched: the frame is not read.
   const uint32_t c0 = ck & 0xffffu, k = ck >> 16;
   const uint32_t c = (~fold32(((~c0) & 0xffffu) + port)) & 0xffffu;
+  // (the fused kernel wrote the frame and its stash: k <= 2, the TCP header
+  // inside the output arena; checked all the same, a bad stash must not
+  // turn into a stray store)
+  if (k > 2u || (uint64_t)o_off + 52u + 4u * k > a.out_arena_len) return;
   uint8_t *tcp = a.out_arena + o_off + 34u + 4u * k;  // the TCP header
 #ifdef CGPU_NAT64_ABL_NOPATCHSTORE  // timing ablation only: the frames are not patched
   if (c == 0x12345u) tcp[0] = 0;
