@@ -71,6 +71,13 @@ constexpr uint32_t kRowMaxLen = CGPU_PARSE_ROW_MAX;  // the rows path: frames up
 #ifndef CGPU_RECON_WHOLE
 #define CGPU_RECON_WHOLE 0
 #endif
+// reconcile: frames 16-B aligned and at least 64 B long get their first 64 B
+// stored four lanes per frame, so that one store instruction writes whole
+// 64-B pieces of 16 frames (full sectors in 64-B slots) instead of each lane
+// storing 2-B fields into its own frame's sector (0: field stores only).
+#ifndef CGPU_RECON_LDS
+#define CGPU_RECON_LDS 1
+#endif
 
 __device__ __forceinline__ uint32_t sel3(uint32_t k, uint32_t a, uint32_t b, uint32_t c) {
   return k == 0u ? a : (k == 1u ? b : c);
@@ -1049,16 +1056,15 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     if (l4_c == swap16(stored_le)) meta |= CGPU_META_L4_CSUM_OK;
   }
 
-  if (!valid) return;
   if constexpr (RECON) {
     // reconcile_all from the held layer outward: L4 (udp.rs:350-354,
     // tcp.rs:619-621, icmp/v4/mod.rs:246, icmp/v6/mod.rs:260), the
     // extension header (nothing), then L3 (v4.rs:486-489, v6/mod.rs:331-334)
-    const bool rec = L4C ? l4_ok
-                         : (a.depth >= CGPU_LAYER_L3 ? l3_ok : eth_ok && ((mi >> 8) & 0xffu) != 0u);
+    const bool rec = valid && (L4C ? l4_ok
+                                   : (a.depth >= CGPU_LAYER_L3 ? l3_ok : eth_ok && ((mi >> 8) & 0xffu) != 0u));
+    // the fields reconcile writes: frame position and big-endian value
+    uint32_t fp[4], fv[4], nf = 0;
     if (rec) {
-      // the fields reconcile writes: frame position and big-endian value
-      uint32_t fp[4], fv[4], nf = 0;
       if (L4C) {
         if (udp) {
           fp[0] = l4_off + 4u;
@@ -1083,14 +1089,52 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
           fv[nf++] = ip_c;
         }
       }
-      uint8_t *f = a.wr_arena + off;
+    }
+    uint8_t *f = a.wr_arena + off;
+    bool stored = false;  // the fields below byte 64 went out with the whole 64 B
+#if CGPU_RECON_LDS
+    // Whole waves only (every lane holds a packet: each lane stores chunks of
+    // other lanes' frames).  A frame goes out this way if it is reconciled,
+    // 16-B aligned and at least 64 B long; its first 64 B are the window P
+    // with the fields patched in.
+    const bool whole = rec && (off & 15u) == 0u && len >= 64u && (uint64_t)off + 64u <= a.arena_len;
+    if (__builtin_amdgcn_read_exec() == ~0ull && __ballot(whole)) {
+      // four rounds of 16 frames: lane l re-reads chunk l & 3 of the round's
+      // frame l >> 2 (an L2 hit: the window loaded that line a moment ago;
+      // keeping the window in registers through the sums spilled), patches
+      // the fields that fall into it (positions and values from the frame's
+      // lane by shuffles) and stores it: one instruction writes the first
+      // 64 B of 16 frames, whole sectors in 64-B slots
+      const uint32_t lane = threadIdx.x & 63u;
+      const uint64_t wm = __ballot(whole);
+      uint32_t pf[4];  // field: position << 16 | big-endian value (none: 0xffff0000)
+#pragma unroll
+      for (uint32_t q = 0; q < 4u; ++q) pf[q] = whole && q < nf && fp[q] < 64u ? (fp[q] << 16) | fv[q] : 0xffff0000u;
+      const rsrc_t ws = make_rsrc(a.wr_arena, a.arena_len);
+#pragma unroll
+      for (uint32_t r = 0; r < 4u; ++r) {
+        const uint32_t fr = 16u * r + (lane >> 2), c = lane & 3u;  // the wave's frame, its chunk
+        const uint32_t foff = (uint32_t)__shfl((int)off, (int)fr);
+        const bool fw = (wm >> fr) & 1ull;
+        u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(ws, (int)(fw ? foff + 16u * c : kNoRead), 0, 0);
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; ++q) {
+          const uint32_t f = (uint32_t)__shfl((int)pf[q], (int)fr), pos = f >> 16, val = swap16(f & 0xffffu);
+#pragma unroll
+          for (uint32_t j = 0; j < 4u; ++j)
+            if (pos == 16u * c + 4u * j || pos == 16u * c + 4u * j + 2u)
+              v[j] = (pos & 2u) ? ((v[j] & 0xffffu) | (val << 16)) : ((v[j] & 0xffff0000u) | val);
+        }
+        if (fw) __builtin_amdgcn_raw_buffer_store_b128(v, ws, (int)(foff + 16u * c), 0, 0);
+      }
+      stored = whole;
+    }
+#endif
+    if (rec) {
 #if CGPU_RECON_WHOLE
       // A dword-aligned frame of 64 B or more gets its first 64 bytes back
-      // whole (the window with the fields patched in: whole 16-B chunks, a
-      // fully written 64-B sector for frames in 64-B slots) instead of 2-B
-      // stores into partly written sectors; fields past byte 64 (IPv6 behind
-      // tags / TCP) are stored alone.
-      if ((off & 3u) == 0u && len >= 64u) {
+      // whole from its own lane (four 16-B stores into its sector).
+      if (!stored && (off & 3u) == 0u && len >= 64u) {
         uint32_t W[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) W[j] = P[j];
@@ -1108,20 +1152,19 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
         for (int c = 0; c < 4; ++c)
           __builtin_amdgcn_raw_buffer_store_b128(u32x4{W[4 * c], W[4 * c + 1], W[4 * c + 2], W[4 * c + 3]}, ws,
                                                  (int)(off + 16u * c), 0, 0);
-#pragma unroll
-        for (uint32_t q = 0; q < 4u; ++q)
-          if (q < nf && fp[q] >= 64u) st16be(f + fp[q], fv[q]);
-      } else
-#endif
-      {
-#pragma unroll
-        for (uint32_t q = 0; q < 4u; ++q)
-          if (q < nf) st16be(f + fp[q], fv[q]);
+        stored = true;
       }
+#endif
+      // the fields not yet stored (all of them, or those past byte 64: IPv6
+      // behind tags, its TCP checksum)
+#pragma unroll
+      for (uint32_t q = 0; q < 4u; ++q)
+        if (q < nf && (!stored || fp[q] >= 64u)) st16be(f + fp[q], fv[q]);
     }
-    if (a.rstatus != nullptr) a.rstatus[i] = rec ? CGPU_RECON_OK : CGPU_RECON_SKIPPED;
+    if (valid && a.rstatus != nullptr) a.rstatus[i] = rec ? CGPU_RECON_OK : CGPU_RECON_SKIPPED;
     return;
   }
+  if (!valid) return;
   a.meta[i] = meta;
   if ((IPC || L4C) && a.csum != nullptr) a.csum[i] = ip_c | (l4_c << 16);
 
