@@ -75,8 +75,8 @@ constexpr uint32_t kRowMaxLen = CGPU_PARSE_ROW_MAX;  // the rows path: frames up
 // stored four lanes per frame, so that one store instruction writes whole
 // 64-B pieces of 16 frames (full sectors in 64-B slots) instead of each lane
 // storing 2-B fields into its own frame's sector (0: field stores only).
-#ifndef CGPU_RECON_LDS
-#define CGPU_RECON_LDS 1
+#ifndef CGPU_RECON_COAL
+#define CGPU_RECON_COAL 1
 #endif
 
 __device__ __forceinline__ uint32_t sel3(uint32_t k, uint32_t a, uint32_t b, uint32_t c) {
@@ -1092,7 +1092,7 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
     }
     uint8_t *f = a.wr_arena + off;
     bool stored = false;  // the fields below byte 64 went out with the whole 64 B
-#if CGPU_RECON_LDS
+#if CGPU_RECON_COAL
     // Whole waves only (every lane holds a packet: each lane stores chunks of
     // other lanes' frames).  A frame goes out this way if it is reconciled,
     // 16-B aligned and at least 64 B long; its first 64 B are the window P
