@@ -731,7 +731,9 @@ __device__ __forceinline__ void defer_append(const Nat64Args &a, uint32_t lane, 
   (void)i;
   const uint64_t dm = __ballot(flag);
   if (!dm) return;
+#ifndef CGPU_NAT64_ABL_NOFLAG  // timing ablation only (cold batches): no flag, the tail always runs
   if (lane == (uint32_t)__builtin_ctzll(dm)) a.pm.state[4u + a.par] = 1u;
+#endif
 }
 
 // The general path: one quad per frame (any alignment, any length); `i` is
@@ -1466,7 +1468,9 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   __shared__ uint32_t s_wc[kOrderU][kBlock / 64];
   uint32_t *const st = a.pm.state;
   if (blockIdx.x == 0 && threadIdx.x == 0) st[4u + (a.par ^ 1u)] = 0u;  // the previous call's flag
+#ifndef CGPU_NAT64_ABL_NOFLAG
   if (st[4u + a.par] == 0u) return;  // nothing deferred: no new key
+#endif
   uint32_t *const cnt = a.chunks, *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
   uint32_t *const mism = a.chunks + 10u * nb;  // the tag collisions (packet indices)
   const TailCtl ctl = tail_ctl(a);
@@ -1599,7 +1603,9 @@ __device__ __forceinline__ void patch_packet(const Nat64Args &a, uint32_t i, uin
 }
 
 __global__ __launch_bounds__(kBlock) void nat64_tail_patch(Nat64Args a, uint32_t nb) {
+#ifndef CGPU_NAT64_ABL_NOFLAG
   if (a.pm.state[4u + a.par] == 0u) return;  // nothing deferred: no new key
+#endif
   const uint32_t *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
   const uint32_t port_base = tail_ctl(a).top[2];
   for (uint32_t c = blockIdx.x; c < nb; c += gridDim.x) {
