@@ -1234,13 +1234,8 @@ __device__ __forceinline__ void chunks_firsts(const Nat64Args &a, uint32_t c0, u
     const bool f = !bad[j] && w7[j] == i;
     const uint64_t m = __ballot(f);
     if (lane == 0 && c < nb) {
-#ifdef CGPU_NAT64_ABL_PLAINST  // timing ablation only (the last arriver may read stale counts)
-      cmask[8u * c + 2u * wave] = (uint32_t)m;
-      cmask[8u * c + 2u * wave + 1u] = (uint32_t)(m >> 32);
-#else
       st_sc1(&cmask[8u * c + 2u * wave], (uint32_t)m);
       st_sc1(&cmask[8u * c + 2u * wave + 1u], (uint32_t)(m >> 32));
-#endif
       s_wc[j][wave] = (uint32_t)__popcll(m);
     }
     const uint64_t bm = __ballot(bad[j]);
@@ -1258,11 +1253,7 @@ __device__ __forceinline__ void chunks_firsts(const Nat64Args &a, uint32_t c0, u
     uint32_t t = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kBlock / 64u; ++w) t += s_wc[threadIdx.x][w];
-#ifdef CGPU_NAT64_ABL_PLAINST
-    if (c < nb) cnt[c] = t;
-#else
     if (c < nb) st_sc1(&cnt[c], t);
-#endif
   }
   __syncthreads();  // s_wc is reused
 }
@@ -1479,10 +1470,8 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   // write-through stores: no atomics of their own
   const unsigned long long ts = wall_clock64();
 #endif
-#ifndef CGPU_NAT64_ABL_NOCHUNKS  // timing ablation only: the arrival and the scan alone
   for (uint32_t c0 = blockIdx.x; c0 < nb; c0 += kOrderU * gridDim.x)
     chunks_firsts(a, c0, gridDim.x, nb, cnt, cmask, mism, ctl, s_wc);
-#endif
 #ifdef CGPU_NAT64_TAIL_CLOCK
   if (threadIdx.x == 0) {
     __hip_atomic_store(&g_clk[2 * blockIdx.x], ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1968,13 +1957,6 @@ __global__ void portmap_init(PortMapDev pm, uint32_t first_port) {
   }
 }
 
-#ifdef CGPU_NAT64_DIAG_GAP_US
-__global__ void diag_spin(unsigned long long ticks) {  // wall clock: 100 MHz
-  const unsigned long long t0 = wall_clock64();
-  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
-}
-#endif
-
 }  // namespace
 
 uint32_t nat64_num_blocks(uint32_t n) { return (n + kBlock - 1) / kBlock; }
@@ -2003,9 +1985,6 @@ hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s, hipEvent_t done)
   return hipGetLastError();
 #endif
   hipLaunchKernelGGL(nat64_6to4_fused, dim3(nbf), dim3(kBlock), 0, s, a);
-#ifdef CGPU_NAT64_DIAG_GAP_US  // diagnosis only: an idle gap between the fused kernel and the tail
-  hipLaunchKernelGGL(diag_spin, dim3(1), dim3(64), 0, s, (unsigned long long)(CGPU_NAT64_DIAG_GAP_US) * 100ull);
-#endif
   // the tail: the order of the new keys, then their frames' ports; in the
   // steady state (no new key) both grids return at once
   const uint32_t og = (nb + kOrderU - 1u) / kOrderU;
