@@ -282,11 +282,19 @@ __device__ __forceinline__ void ipv4_header(const V6 &v, uint32_t len, uint32_t 
 // words were written by an earlier launch).  refs only ever go 0 -> (i + 1)
 // -> kPersist, and a claim's tag never changes, so a stale probe load at
 // worst leads to the CAS, which returns the coherent word.
+#ifndef CGPU_NAT64_LAZY_TAG
+#define CGPU_NAT64_LAZY_TAG 1
+#endif
 __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i,
                                                   const uint32_t (&key)[5], uint32_t h, u32x4 s0,
                                                   u32x4 s1, uint32_t &port) {
   port = 0xffffffffu;
+#if CGPU_NAT64_LAZY_TAG
+  uint32_t tag = 0;  // computed when a slot is not a committed key (never in the steady state)
+  bool have_tag = false;
+#else
   const uint32_t tag = key_tag(key) & a.pm.tag_mask;
+#endif
   for (uint32_t probe = 0; probe <= a.pm.cap_mask; ++probe) {
     if (probe != 0u) {  // the first slot was loaded by the caller
       const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
@@ -295,6 +303,12 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
     }
     uint32_t *w = a.pm.slots[h].w;
     uint32_t ref = s0[0], stag = s0[1];
+#if CGPU_NAT64_LAZY_TAG
+    if (!(ref & kPersist) && !have_tag) {
+      tag = key_tag(key) & a.pm.tag_mask;
+      have_tag = true;
+    }
+#endif
     if (ref == 0u) {
       const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long *>(w), 0ull,
                                                (unsigned long long)(i + 1u) |
@@ -1058,7 +1072,9 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     *reinterpret_cast<u32x4 *>(rec + 16) =
         u32x4{act ? nl : 0u, payload + accA, ph | (k << 16), o_off};
     // a deferred frame's checksum (with port 0) and VLAN depth, for the tail
+#ifndef CGPU_NAT64_ABL_NOSTASHC0  // timing ablation only (steady state): without the stash store
     if (deferred) a.stash_c0[i] = ((~fold32(ph + swap16(fold32(payload + accA)))) & 0xffffu) | (k << 16);
+#endif
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #ifndef CGPU_NAT64_ABL_NOREWRITE
@@ -1458,7 +1474,9 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   __shared__ uint32_t s_part[kBlock / 64];
   __shared__ uint32_t s_wc[kOrderU][kBlock / 64];
   uint32_t *const st = a.pm.state;
-  if (blockIdx.x == 0 && threadIdx.x == 0) st[4u + (a.par ^ 1u)] = 0u;  // the previous call's flag
+  // the previous call's flag, cleared only if set: in the steady state the
+  // flag line is never written, so every workgroup's read of it can hit
+  if (blockIdx.x == 0 && threadIdx.x == 0 && st[4u + (a.par ^ 1u)] != 0u) st[4u + (a.par ^ 1u)] = 0u;
 #ifndef CGPU_NAT64_ABL_NOFLAG
   if (st[4u + a.par] == 0u) return;  // nothing deferred: no new key
 #endif
