@@ -63,6 +63,20 @@ __global__ __launch_bounds__(256) void write_clk(u32x4 *p, size_t n16, unsigned 
   }
 }
 
+// 64 B per lane (one frame in a 64-B slot): read it and write it back in
+// place, or write it to another buffer (the reconcile kernel's store pattern
+// against a copy's).
+__global__ __launch_bounds__(256) void rmw64(u32x4 *p, u32x4 *q, size_t nframes) {
+  const size_t f = blockIdx.x * 256ull + threadIdx.x;
+  if (f >= nframes) return;
+  u32x4 v[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) v[c] = p[4 * f + c];
+  v[1][0] ^= 0x00010000u;  // change a field (a 2-B store's worth)
+#pragma unroll
+  for (int c = 0; c < 4; ++c) q[4 * f + c] = v[c];
+}
+
 __global__ __launch_bounds__(256) void empty(const uint32_t *flag, uint32_t *out) {
   if (*flag == 0u) return;  // the steady state: nothing deferred
   out[blockIdx.x * 256 + threadIdx.x] = 1u;
@@ -170,6 +184,34 @@ int main() {
       }
     }
     CK(hipFree(clk));
+  }
+  // 1 Mi 64-B frames: in place vs into another buffer, rotating over 4
+  // copies (256 MiB, past the 256 MiB MALL with the second buffer)
+  {
+    const size_t nf = 1u << 20, fb = nf * 64;
+    u32x4 *src, *dst;
+    CK(hipMalloc(&src, 4 * fb));
+    CK(hipMalloc(&dst, 4 * fb));
+    CK(hipMemset(src, 3, 4 * fb));
+    for (int mode = 0; mode < 2; ++mode) {
+      for (int rep = 0; rep < 2; ++rep) {
+        CK(hipEventRecord(a, s));
+        for (int it = 0; it < iters; ++it) {
+          u32x4 *p = src + (it & 3) * (fb / 16);
+          u32x4 *q = mode ? dst + (it & 3) * (fb / 16) : p;
+          hipLaunchKernelGGL(rmw64, dim3(nf / 256), dim3(256), 0, s, p, q, nf);
+        }
+        CK(hipEventRecord(b, s));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (rep == 1)
+          printf("1 Mi x 64 B, 64 B per lane, %s: %.2f us per launch (%.0f GB/s read + write)\n",
+                 mode ? "into another buffer" : "in place", ms * 1e3 / iters, 2.0 * fb / (ms * 1e-3 / iters) / 1e9);
+      }
+    }
+    CK(hipFree(src));
+    CK(hipFree(dst));
   }
   // stream ids: are they reused after a destroy (the nat64 map's "same
   // stream as the previous call" test must not be fooled by a new stream
