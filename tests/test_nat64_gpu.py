@@ -453,3 +453,23 @@ def test_claim_tag_collisions_repaired(ctx, monkeypatch, mask):
     o6 = (np.arange(len(ro), dtype=np.int64) * 256).astype(np.uint32)
     _nat_both(ctx, gw, pm, "4to6", ra, ro, rl, o6, 256 * len(ro) + 64)
     gw.close()
+
+
+def test_cold_batch_past_the_tails_single_round(ctx):
+    """A cold batch of 1,060,921 frames: 4,145 chunks of 256 packets, more
+    than the order launch's 1,024 workgroups x 4 chunks and the patch
+    launch's 4,096 workgroups cover in one round (both loop), and more than
+    the 16 counts per thread the last workgroup's scan keeps in registers
+    (it reads them one by one).  Small frames keep the arena at 100 MB.
+    Every byte, length, disposition, status and the map state against the
+    oracle; then the same batch again, every key committed."""
+    from capsule_amd import packets
+
+    n = 4145 * 256 - 14199
+    gw = packets.Nat64Gateway(ctx)  # 2^20 slots
+    pm = oracle_lib.PortMap()
+    a, o, l = synth.nat64_stream(n, frame_len=96, n_keys=60_000, seed=91, drop_frac=0.02)
+    for _ in range(2):
+        _nat_both(ctx, gw, pm, "6to4", a, o, l, o, len(a) + 64)
+        assert gw.size() == pm.size() and gw.next_port() == pm.next_port()
+    gw.close()
