@@ -764,6 +764,9 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   DeviceGuard dg(ctx->device);
   if (!dg.ok()) return fail(CGPU_ENODEV);
   if (pm->scratch_n < in->n) {
+    // the map's previous call (any stream) may still be using the old
+    // scratch: wait for it before the scratch is freed and replaced
+    if (pm->pkt_slot && hipEventSynchronize(pm->done) != hipSuccess) return fail(CGPU_EIO);
     if (pm->pkt_slot) (void)hipFree(pm->pkt_slot);
     pm->pkt_slot = nullptr;
     pm->scratch_n = 0;
