@@ -285,9 +285,6 @@ __device__ __forceinline__ void ipv4_header(const V6 &v, uint32_t len, uint32_t 
 #ifndef CGPU_NAT64_LAZY_TAG
 #define CGPU_NAT64_LAZY_TAG 1
 #endif
-#ifndef CGPU_NAT64_LATE_CLAIM  // rows path: claims and joins after the frames' stores (probe_committed)
-#define CGPU_NAT64_LATE_CLAIM 1
-#endif
 __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i,
                                                   const uint32_t (&key)[5], uint32_t h, u32x4 s0,
                                                   u32x4 s1, uint32_t &port) {
@@ -340,39 +337,6 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
       a.stash_port[i] = (uint16_t)key[4];
       if (s1[3] > i) atomicMin(&w[7], i);
       return h | kLocalBit;
-    }
-    h = (h + 1u) & a.pm.cap_mask;
-  }
-  return kNoSlot;
-}
-
-// The late claim (rows path, cold batches): the lookup walks only the
-// committed slots of the key's chain with the plain loads it has; at the
-// first slot that is not a committed key (empty, or claimed in this batch)
-// the key is known to be new -- a committed key is never behind such a slot:
-// it sits at the first slot that was free when it was committed, and no slot
-// is ever freed -- so its frame is written with port 0 at once and the
-// claim or join (atomics, a returning CAS) is made after the frame's stores,
-// off the wave's path to them.  Returns the slot of a committed match (port
-// set), kPendSlot with `hc` the slot to claim from, or kNoSlot.
-constexpr uint32_t kPendSlot = 0xfffffffeu;
-__device__ __forceinline__ uint32_t probe_committed(const Nat64Args &a, const uint32_t (&key)[5], uint32_t h,
-                                                   u32x4 s0, u32x4 s1, uint32_t &port, uint32_t &hc) {
-  port = 0xffffffffu;
-  for (uint32_t probe = 0; probe <= a.pm.cap_mask; ++probe) {
-    if (probe != 0u) {
-      const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
-      s0 = sp[0];
-      s1 = sp[1];
-    }
-    if (!(s0[0] & kPersist)) {
-      hc = h;
-      return kPendSlot;
-    }
-    const uint32_t other[5] = {s0[2], s0[3], s1[0], s1[1], s1[2] & 0xffffu};
-    if (key_eq(key, other)) {
-      port = s1[2] >> 16;
-      return h;
     }
     h = (h + 1u) & a.pm.cap_mask;
   }
@@ -1063,23 +1027,13 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   else rows_payload<false>(X, lds, row, l, nl0);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   // A4: assigned_port (main.rs:41-53), the IPv4 header
-  uint32_t slot = kNoSlot, port = 0xffffffffu, hc = kNoSlot;
-#if CGPU_NAT64_LATE_CLAIM
-  // the claims of this batch cannot fill the map (entries + n <= capacity):
-  // a chain always has a slot left, so no frame written before its claim can
-  // turn out to be TABLE_FULL
-  const bool late = (uint64_t)a.pm.state[1] + a.n <= (uint64_t)a.pm.cap_mask + 1u;
-#endif
+  uint32_t slot = kNoSlot, port = 0xffffffffu;
   if (act0) {
 #ifdef CGPU_NAT64_ABL_NOPROBE
     slot = 0u;
     port = 1025u;
 #else
-#if CGPU_NAT64_LATE_CLAIM
-    if (late) slot = probe_committed(a, key, h, s0, s1, port, hc);
-    else
-#endif
-      slot = probe_port_at(a, i, key, h, s0, s1, port);
+    slot = probe_port_at(a, i, key, h, s0, s1, port);
 #endif
   }
   if (v.disp == CGPU_ACT && slot == kNoSlot) {
@@ -1095,7 +1049,7 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   const bool deferred = act && !now;
   if (valid) {
     a.out_len[i] = act ? (uint16_t)nl : 0;
-    if (slot != kPendSlot) a.pkt_slot[i] = now ? kNoSlot : slot;  // (a late claim stores it below)
+    a.pkt_slot[i] = now ? kNoSlot : slot;
     a.disposition[i] = (uint8_t)v.disp;
     a.status[i] = (uint8_t)v.st;
   }
@@ -1125,15 +1079,6 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #ifndef CGPU_NAT64_ABL_NOREWRITE
   rows_store(a, ors, X, lds, row, l);
-#endif
-#if CGPU_NAT64_LATE_CLAIM
-  // the late claims and joins, behind the frames' stores (the slot reloaded:
-  // probe_port_at takes stale words and settles them with its CAS)
-  if (__ballot(slot == kPendSlot) && slot == kPendSlot) {
-    const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[hc]);
-    uint32_t p2;
-    a.pkt_slot[i] = probe_port_at(a, i, key, hc, sp[0], sp[1], p2);  // never kNoSlot here (see `late`)
-  }
 #endif
   return true;
 }
