@@ -241,7 +241,7 @@ def cpu_baseline(w, seconds):
         if w["kind"] == "reconcile":
             work = arena.copy()
             meta = w["meta"]
-            return lambda: L.or_reconcile(p(work), p(off), p(ln), p(meta), n, w["flags"], 4, None)
+            return lambda: L.or_reconcile(p(work), len(work), p(off), p(ln), p(meta), n, w["flags"], 4, None)
         pm = oracle_lib.PortMap()
         out = np.zeros(len(arena), np.uint8)
         olen = np.zeros(n, np.uint16)

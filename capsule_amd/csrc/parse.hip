@@ -545,6 +545,18 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
       for (int j = 16; j < kWin; ++j) P[j] = 0u;
     }
   }
+#if CGPU_PARSE_ROWS && CGPU_RECON_COAL
+  if constexpr (RECON && ROWS) {
+    // the window's first 64 B, for the coalesced store at the end (the
+    // wave's LDS is free once the prologue has handed the windows over)
+    static_assert(kPathLds >= 64u * 16u, "a 64-B window per lane");
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    uint32_t *pl = &rlds[threadIdx.x >> 6][16u * (threadIdx.x & 63u)];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      *reinterpret_cast<u32x4 *>(pl + 4 * m) = u32x4{P[4 * m], P[4 * m + 1], P[4 * m + 2], P[4 * m + 3]};
+  }
+#endif
 
   // --- Ethernet: VLAN marker at bytes 12-13 (ethernet.rs:164-181) ---------
   const uint32_t marker = be16_lo(P[3]);
@@ -1060,7 +1072,10 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
     // reconcile_all from the held layer outward: L4 (udp.rs:350-354,
     // tcp.rs:619-621, icmp/v4/mod.rs:246, icmp/v6/mod.rs:260), the
     // extension header (nothing), then L3 (v4.rs:486-489, v6/mod.rs:331-334)
-    const bool rec = valid && (L4C ? l4_ok
+    // a frame not wholly inside the arena (a descriptor against the ABI's
+    // precondition, or stale meta) is skipped, never written past the end
+    const bool rec = valid && (uint64_t)off + len <= (uint64_t)a.arena_len &&
+                     (L4C ? l4_ok
                                    : (a.depth >= CGPU_LAYER_L3 ? l3_ok : eth_ok && ((mi >> 8) & 0xffu) != 0u));
     // the fields reconcile writes: frame position and big-endian value
     uint32_t fp[4], fv[4], nf = 0;
@@ -1099,24 +1114,34 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
     // with the fields patched in.
     const bool whole = rec && (off & 15u) == 0u && len >= 64u && (uint64_t)off + 64u <= a.arena_len;
     if (__builtin_amdgcn_read_exec() == ~0ull && __ballot(whole)) {
-      // four rounds of 16 frames: lane l re-reads chunk l & 3 of the round's
-      // frame l >> 2 (an L2 hit: the window loaded that line a moment ago;
-      // keeping the window in registers through the sums spilled), patches
-      // the fields that fall into it (positions and values from the frame's
-      // lane by shuffles) and stores it: one instruction writes the first
-      // 64 B of 16 frames, whole sectors in 64-B slots
+      // four rounds of 16 frames: lane l takes chunk l & 3 of the round's
+      // frame l >> 2, patches the fields that fall into it (positions and
+      // values from the frame's lane by shuffles) and stores it: one
+      // instruction writes the first 64 B of 16 frames, whole sectors in
+      // 64-B slots.  The chunk comes from the copy of the window the rows
+      // variant staged in LDS (below the loads); the window variant re-reads
+      // it (an L2 hit there: the window loaded that line a moment ago, while
+      // a long frame's first line has left the L2 by the time its tail is
+      // summed; keeping the window in registers through the sums spilled)
       const uint32_t lane = threadIdx.x & 63u;
       const uint64_t wm = __ballot(whole);
       uint32_t pf[4];  // field: position << 16 | big-endian value (none: 0xffff0000)
 #pragma unroll
       for (uint32_t q = 0; q < 4u; ++q) pf[q] = whole && q < nf && fp[q] < 64u ? (fp[q] << 16) | fv[q] : 0xffff0000u;
       const rsrc_t ws = make_rsrc(a.wr_arena, a.arena_len);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #pragma unroll
       for (uint32_t r = 0; r < 4u; ++r) {
         const uint32_t fr = 16u * r + (lane >> 2), c = lane & 3u;  // the wave's frame, its chunk
         const uint32_t foff = (uint32_t)__shfl((int)off, (int)fr);
         const bool fw = (wm >> fr) & 1ull;
-        u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(ws, (int)(fw ? foff + 16u * c : kNoRead), 0, 0);
+        u32x4 v;
+#if CGPU_PARSE_ROWS
+        if (ROWS)
+          v = *reinterpret_cast<const u32x4 *>(&rlds[threadIdx.x >> 6][16u * fr + 4u * c]);
+        else
+#endif
+          v = __builtin_amdgcn_raw_buffer_load_b128(ws, (int)(fw ? foff + 16u * c : kNoRead), 0, 0);
 #pragma unroll
         for (uint32_t q = 0; q < 4u; ++q) {
           const uint32_t f = (uint32_t)__shfl((int)pf[q], (int)fr), pos = f >> 16, val = swap16(f & 0xffffu);
@@ -1175,6 +1200,184 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
   parse_body<IPC, L4C, HASH, FIELDS, EXT, V4U, ROWS, RECON>(a);
 }
 
+// ---- reconcile_all of short frames without a re-parse ----------------------
+// The general RECON body above runs the whole parse machinery again (window
+// paths, classification, status chain) although the meta word already holds
+// every layer and offset.  A wave whose reconciled frames are all 16-B
+// aligned, at most 64 B long and of one layout (VLAN depth, IPv4/IPv6,
+// UDP/TCP/ICMP) takes this path instead: the layout is a compile-time
+// constant, so every field position and sum range is fixed; a lane loads its
+// frame (four 16-B loads), writes the new length fields and zeroed checksum
+// fields into its registers first (reconcile's order: udp.rs:350-354 sets the
+// length before the checksum; v4.rs:486-489 the total_length before the header
+// checksum), sums the L4 span with the pseudo-header addresses and the IPv4
+// header from those registers, patches the checksums in and stores the 16-B
+// chunks that hold a field.  Frames in any other shape take the general body.
+
+// Halfword at frame byte POS (even) of the little-endian window, set to the
+// wire bytes of big-endian value v.
+template <uint32_t POS>
+__device__ __forceinline__ void set_be16(uint32_t (&P)[16], uint32_t v) {
+  static_assert(POS % 2u == 0u && POS < 64u, "an even position in the window");
+  const uint32_t le = swap16(v & 0xffffu);
+  P[POS / 4u] = (POS & 2u) ? ((P[POS / 4u] & 0xffffu) | (le << 16)) : ((P[POS / 4u] & 0xffff0000u) | le);
+}
+
+// Bytes of dword j that lie in [A, B) (compile-time bounds).
+constexpr uint32_t range_mask(uint32_t j, uint32_t A, uint32_t B) {
+  uint32_t m = 0;
+  for (uint32_t b = 0; b < 4u; ++b)
+    if (4u * j + b >= A && 4u * j + b < B) m |= 0xffu << (8u * b);
+  return m;
+}
+
+// u16-word sum (little-endian domain) of window bytes [A, min(B, end)).
+template <uint32_t A, uint32_t B>
+__device__ __forceinline__ uint32_t sum_range(const uint32_t (&P)[16], uint32_t end, uint32_t acc) {
+#pragma unroll
+  for (uint32_t j = A / 4u; j < (B + 3u) / 4u; ++j) {
+    acc = sad16(P[j] & (range_mask(j, A, B) & end_mask((int)j, end)), acc);
+  }
+  return acc;
+}
+
+template <uint32_t K, bool V6, uint32_t L4T>
+__device__ __forceinline__ void recon_short_frames(rsrc_t rs, rsrc_t ws, bool rec, uint32_t off, uint32_t len,
+                                                   uint32_t rec_lane) {
+  constexpr uint32_t E = 14u + 4u * K;             // Ethernet header_len (ethernet.rs:253-261)
+  constexpr uint32_t L4 = E + (V6 ? 40u : 20u);    // the fixed L3 header sizes
+  constexpr bool UDP = L4T == CGPU_L4_UDP, TCP = L4T == CGPU_L4_TCP, ICMP4 = !V6 && L4T == CGPU_L4_ICMP;
+  constexpr uint32_t CS = L4 + (UDP ? 6u : (TCP ? 16u : 2u));  // the L4 checksum field
+  // the L4 sum's bytes: pseudo-header addresses + the span [L4, len), one
+  // contiguous range (ICMPv4 has no pseudo-header, icmp/v4/mod.rs:118-129)
+  constexpr uint32_t A = ICMP4 ? L4 : (V6 ? E + 8u : E + 12u);
+  constexpr uint32_t PROTO = UDP ? 17u : (TCP ? 6u : 58u);
+  // a layout whose headers end past byte 64 has no frame on this path
+  // (recon_short requires the headers inside a frame of at most 64 B)
+  if constexpr (L4 + (UDP ? 8u : (TCP ? 20u : 4u)) > 64u) {
+    return;
+  } else {
+  uint32_t P[16];
+#pragma unroll
+  for (uint32_t c = 0; c < 4u; ++c) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(rec && 16u * c < len ? off + 16u * c : kNoRead), 0, 0);
+    P[4 * c] = v[0];
+    P[4 * c + 1] = v[1];
+    P[4 * c + 2] = v[2];
+    P[4 * c + 3] = v[3];
+  }
+  const uint32_t span = len - L4;  // Udp/Tcp::len(): data_len - offset
+  if constexpr (UDP) set_be16<L4 + 4u>(P, span);
+  set_be16<CS>(P, 0u);
+  if constexpr (V6) {
+    set_be16<E + 4u>(P, len - E - 40u);  // payload_length (v6/mod.rs:331-334)
+  } else {
+    set_be16<E + 2u>(P, len - E);  // total_length (v4.rs:486-489)
+    set_be16<E + 10u>(P, 0u);
+  }
+  // the span ends at the frame's end: a scalar bound when the wave's frames
+  // share one length
+  const uint32_t ulen = __builtin_amdgcn_readlane(len, (int)rec_lane);
+  uint32_t s;
+  if (!__ballot(rec && len != ulen)) s = sum_range<A, 64u>(P, ulen, 0u);
+  else s = sum_range<A, 64u>(P, len, 0u);
+  uint32_t l4_c = ICMP4 ? (~swap16(fold32(s))) & 0xffffu : (~fold32(swap16(fold32(s)) + span + PROTO)) & 0xffffu;
+  if (UDP && l4_c == 0u) l4_c = 0xffffu;  // udp.rs:137-140
+  set_be16<CS>(P, l4_c);
+  constexpr uint32_t IPCS = E + 10u;
+  if constexpr (!V6) {
+    const uint32_t si = sum_range<E, E + 20u>(P, 64u, 0u);
+    set_be16<IPCS>(P, (~swap16(fold32(si))) & 0xffffu);
+  }
+  // the chunks holding a field: whole 16-B stores where the chunk lies
+  // inside the frame, else the fields as 2-B stores
+  constexpr uint32_t F0 = V6 ? E + 4u : E + 2u, F1 = V6 ? E + 4u : IPCS, F2 = UDP ? L4 + 4u : CS, F3 = CS;
+  constexpr uint32_t cmask = (1u << (F0 / 16u)) | (1u << (F1 / 16u)) | (1u << (F2 / 16u)) | (1u << (F3 / 16u));
+  if (!rec) return;
+#pragma unroll
+  for (uint32_t c = 0; c < 4u; ++c) {
+    if (!((cmask >> c) & 1u)) continue;
+    if (16u * c + 16u <= len) {
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{P[4 * c], P[4 * c + 1], P[4 * c + 2], P[4 * c + 3]}, ws,
+                                             (int)(off + 16u * c), 0, 0);
+    } else {
+      constexpr uint32_t F[4] = {F0, F1, F2, F3};
+#pragma unroll
+      for (uint32_t q = 0; q < 4u; ++q) {
+        if (F[q] / 16u != c || (q > 0u && F[q] == F[q - 1u])) continue;
+        const uint32_t w = P[F[q] / 4u];
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)((F[q] & 2u) ? w >> 16 : w), ws, (int)(off + F[q]), 0, 0);
+      }
+    }
+  }
+  }
+}
+
+template <uint32_t K, bool V4U>
+__device__ __forceinline__ void recon_short_k(uint32_t lay, rsrc_t rs, rsrc_t ws, bool rec, uint32_t off,
+                                              uint32_t len, uint32_t rl) {
+  if (V4U || lay == CGPU_L4_UDP) return recon_short_frames<K, false, CGPU_L4_UDP>(rs, ws, rec, off, len, rl);
+  if constexpr (!V4U) {
+    switch (lay) {
+      case CGPU_L4_TCP: return recon_short_frames<K, false, CGPU_L4_TCP>(rs, ws, rec, off, len, rl);
+      case CGPU_L4_ICMP: return recon_short_frames<K, false, CGPU_L4_ICMP>(rs, ws, rec, off, len, rl);
+      case 4u | CGPU_L4_UDP: return recon_short_frames<K, true, CGPU_L4_UDP>(rs, ws, rec, off, len, rl);
+      case 4u | CGPU_L4_TCP: return recon_short_frames<K, true, CGPU_L4_TCP>(rs, ws, rec, off, len, rl);
+      default: return recon_short_frames<K, true, CGPU_L4_ICMP>(rs, ws, rec, off, len, rl);
+    }
+  }
+}
+
+// The short path at depth L4 (wave-uniform decision).  Returns false when
+// the wave has to take the general body; otherwise its frames are done.
+template <bool EXT, bool V4U>
+__device__ __forceinline__ bool recon_short(const ParseArgs &a) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = i < a.n;
+  const uint64_t nb = (uint64_t)a.n;
+  const rsrc_t r_off = make_rsrc(a.off, (uint32_t)(4u * nb < 0xffffffffull ? 4u * nb : 0xffffffffull));
+  const rsrc_t r_len = make_rsrc(a.len, (uint32_t)(2u * nb < 0xffffffffull ? 2u * nb : 0xffffffffull));
+  const rsrc_t r_meta = make_rsrc(a.meta_in, (uint32_t)(4u * nb < 0xffffffffull ? 4u * nb : 0xffffffffull));
+  const uint32_t off = __builtin_amdgcn_raw_buffer_load_b32(r_off, (int)(4u * i), 0, 0);
+  const uint32_t len = __builtin_amdgcn_raw_buffer_load_b16(r_len, (int)(2u * i), 0, 0);
+  const uint32_t mi = __builtin_amdgcn_raw_buffer_load_b32(r_meta, (int)(4u * i), 0, 0);
+  const uint32_t k = (mi & CGPU_META_QINQ) ? 2u : ((mi & CGPU_META_DOT1Q) ? 1u : 0u);
+  const uint32_t m_l3 = (mi >> 16) & 3u, m_l4 = (mi >> 18) & 3u, m_x = (mi >> 24) & 3u;
+  const bool okst = (mi & 0xffu) == CGPU_PKT_OK;
+  // frames behind an IPv6 extension header: the general body (EXT), or not
+  // a packet of the pipeline (no CGPU_F_V6_EXT: no L4 behind the extension)
+  if (EXT && __ballot(valid && okst && m_x != CGPU_EXT_NONE)) return false;
+  // parse_body's reconcile predicate at depth L4: the meta's layers, each in
+  // the accept set, and read_data's bounds (mbuf.rs:313-327) on this length
+  const bool v4 = m_l3 == CGPU_L3_IPV4 && (a.accept & CGPU_F_ACCEPT_V4);
+  const bool v6 = !V4U && m_l3 == CGPU_L3_IPV6 && (a.accept & CGPU_F_ACCEPT_V6);
+  const bool l4in = okst && m_x == CGPU_EXT_NONE;
+  const bool udp = l4in && m_l4 == CGPU_L4_UDP && (a.accept & CGPU_F_ACCEPT_UDP);
+  const bool tcp = !V4U && l4in && m_l4 == CGPU_L4_TCP && (a.accept & CGPU_F_ACCEPT_TCP);
+  const bool icmp = !V4U && l4in && m_l4 == CGPU_L4_ICMP && (a.accept & CGPU_F_ACCEPT_ICMP);
+  const uint32_t l4_end = 14u + 4u * k + (v6 ? 40u : 20u) + (udp ? 8u : (icmp ? 4u : 20u));
+  const bool rec = valid && (v4 || v6) && (udp || tcp || icmp) && l4_end <= len &&
+                   (uint64_t)off + len <= (uint64_t)a.arena_len;
+  const bool fit = (off & 15u) == 0u && len <= 64u && (uint64_t)off + 64u <= (uint64_t)a.arena_len;
+  if (__ballot(rec && !fit)) return false;
+  const uint64_t rm = __ballot(rec);
+  const uint32_t lay = (k << 3) | (v6 ? 4u : 0u) | m_l4;
+  const uint32_t rl = rm ? (uint32_t)__builtin_ctzll(rm) : 0u;
+  const uint32_t lay0 = __builtin_amdgcn_readlane(lay, (int)rl);
+  if (__ballot(rec && lay != lay0)) return false;
+  if (rm) {
+    const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
+    const rsrc_t ws = make_rsrc(a.wr_arena, a.arena_len);
+    switch (lay0 >> 3) {
+      case 0u: recon_short_k<0u, V4U>(lay0 & 7u, rs, ws, rec, off, len, rl); break;
+      case 1u: recon_short_k<1u, V4U>(lay0 & 7u, rs, ws, rec, off, len, rl); break;
+      default: recon_short_k<2u, V4U>(lay0 & 7u, rs, ws, rec, off, len, rl); break;
+    }
+  }
+  if (valid && a.rstatus != nullptr) a.rstatus[i] = rec ? CGPU_RECON_OK : CGPU_RECON_SKIPPED;
+  return true;
+}
+
 // The reconcile kernels: the same body with their own occupancy targets
 // (workgroups of 256 per CU).  The window variant (short frames: every
 // frame's sector is read and written back in place) runs at 6: 45.95
@@ -1186,6 +1389,9 @@ __global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
 #endif
 template <bool L4C, bool EXT, bool V4U>
 __global__ __launch_bounds__(kBlock, CGPU_RECON_WPE_WIN) void recon_kernel(ParseArgs a) {
+  if constexpr (L4C) {
+    if (recon_short<EXT, V4U>(a)) return;
+  }
   parse_body<true, L4C, false, false, EXT, V4U, false, true>(a);
 }
 template <bool L4C, bool EXT, bool V4U>

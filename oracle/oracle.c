@@ -906,15 +906,19 @@ static int recon_accepts(uint32_t flags, uint32_t m, uint32_t depth) {
   return 1;
 }
 
-void or_reconcile(uint8_t *arena, const uint32_t *off, const uint16_t *len, const uint32_t *meta,
-                  uint32_t n, uint32_t flags, uint32_t depth, uint8_t *status) {
+/* A frame not wholly inside the arena (off + len > arena_len: against the
+ * ABI's precondition, or meta left from other descriptors) is skipped, not
+ * written; the reference's Mbuf always holds its data_len bytes. */
+void or_reconcile(uint8_t *arena, uint64_t arena_len, const uint32_t *off, const uint16_t *len,
+                  const uint32_t *meta, uint32_t n, uint32_t flags, uint32_t depth, uint8_t *status) {
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t m = meta[i];
     uint8_t *p = arena + off[i];
     const uint32_t eth = CGPU_META_ETH_LEN(m);
     int done = 0;
-    if (!recon_accepts(flags, m, depth)) {
-      /* a layer outside the parse's accept set: not a packet of this pipeline */
+    if ((uint64_t)off[i] + len[i] > arena_len || !recon_accepts(flags, m, depth)) {
+      /* outside the arena, or a layer outside the parse's accept set: not a
+       * packet of this pipeline */
     } else if (depth == CGPU_LAYER_L4) {
       const uint8_t *seg0;
       int64_t l4_off = -1;

@@ -86,8 +86,8 @@ void or_set_ip(uint8_t *arena, const uint32_t *off, const uint16_t *len, const u
 
 /* Packet::reconcile_all (packets/mod.rs:297-300) at layer `depth` over the
  * packets of a parsed batch, in place; contract of cgpu_reconcile.        */
-void or_reconcile(uint8_t *arena, const uint32_t *off, const uint16_t *len, const uint32_t *meta,
-                  uint32_t n, uint32_t flags, uint32_t depth, uint8_t *status);
+void or_reconcile(uint8_t *arena, uint64_t arena_len, const uint32_t *off, const uint16_t *len,
+                  const uint32_t *meta, uint32_t n, uint32_t flags, uint32_t depth, uint8_t *status);
 
 #ifdef __cplusplus
 }

@@ -61,7 +61,7 @@ def load(name="liboracle.so"):
     L.or_set_ip.restype = None
     L.or_set_ip.argtypes = [vp, vp, vp, vp, u32, vp, u32, vp, u32, vp]
     L.or_reconcile.restype = None
-    L.or_reconcile.argtypes = [vp, vp, vp, vp, u32, u32, u32, vp]
+    L.or_reconcile.argtypes = [vp, u64, vp, vp, vp, u32, u32, u32, vp]
     return L
 
 
@@ -138,16 +138,18 @@ def set_ip(arena, off, length, meta, src=None, dst=None):
     return out, st
 
 
-def reconcile(arena, off, length, meta, flags, depth):
+def reconcile(arena, off, length, meta, flags, depth, arena_len=None):
     """Oracle Packet::reconcile_all at `depth` (3 = L3, 4 = L4) over a parsed
-    batch (arena copied) -> (new arena, status u8[n])."""
+    batch (arena copied) -> (new arena, status u8[n]).  `arena_len`: the
+    arena's length as the device sees it (default: all of `arena`); a frame
+    past it is skipped."""
     n = len(off)
     out = np.array(arena, np.uint8, copy=True)
     off = np.ascontiguousarray(off, np.uint32)
     length = np.ascontiguousarray(length, np.uint16)
     meta = np.ascontiguousarray(meta, np.uint32)
     st = np.zeros(n, np.uint8)
-    lib().or_reconcile(_p(out), _p(off), _p(length), _p(meta), n, flags, depth, _p(st))
+    lib().or_reconcile(_p(out), len(out) if arena_len is None else arena_len, _p(off), _p(length), _p(meta), n, flags, depth, _p(st))
     return out, st
 
 

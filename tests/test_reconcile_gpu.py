@@ -207,3 +207,97 @@ def test_bench_reconcile_config_every_byte(ctx, cfg):
     assert (st.cpu().numpy() == want_st).all()
     assert (want_st == N.RECON_OK).all()
     assert (b.arena.cpu().numpy() == want).all()
+
+
+# ---- the short-frame path (recon_short: frames <= 64 B, 16-B aligned, one
+# layout per wave) and the waves that must leave it for the general body ----
+
+SHORT_KINDS = [synth.V4_UDP, synth.V4_TCP, synth.V4_ICMP, synth.V6_UDP, synth.V6_ICMP]
+
+
+def _short_frames(rng, kind, vlan, lens):
+    hdr = 14 + 4 * vlan + (20 if kind[0] == 4 else 40) + synth.l4_header_len(kind[1])
+    out = []
+    for L in lens:
+        L = max(int(L), hdr)
+        out.append(bytes(synth.build_frames(rng, 1, kind, L, vlan)[0]))
+    return out
+
+
+@pytest.mark.parametrize("vlan", [0, 1, 2])
+@pytest.mark.parametrize("kind", SHORT_KINDS)
+@pytest.mark.parametrize("lens", ["64", "odd", "mixed"])
+def test_short_path_layouts(ctx, vlan, kind, lens):
+    """Every layout the short path instantiates (VLAN depth x IPv4/IPv6 x
+    UDP/TCP/ICMP with headers inside 64 B) at one length per wave (scalar
+    span bound), an odd one (the last byte as byte << 8, checksum.rs:
+    159-166), and per-lane lengths (fields in a chunk that runs past the
+    frame's end take 2-B stores)."""
+    hdr = 14 + 4 * vlan + (20 if kind[0] == 4 else 40) + synth.l4_header_len(kind[1])
+    if hdr > 64:
+        pytest.skip("headers past 64 B: the general body's layout")
+    rng = np.random.default_rng(hash((vlan, kind, lens)) & 0xffff)
+    n = 640 + 37  # ten whole waves and a partial one
+    L = {"64": np.full(n, 64), "odd": np.full(n, 63 if hdr <= 63 else 64),
+         "mixed": rng.integers(hdr, 65, n)}[lens]
+    frames = _short_frames(rng, kind, vlan, L)
+    arena, off, ln = synth.pack_frames(frames)
+    st = gpu_vs_oracle(ctx, arena, off, ln, ALL, N.LAYER_L4, seed=vlan + 3)
+    assert (st == N.RECON_OK).all()
+
+
+def test_short_path_mixed_waves(ctx):
+    """Waves that mix layouts, carry a frame longer than 64 B or an
+    unaligned one (the general body), and waves with unparseable or
+    not-accepted frames among short ones (skipped on the short path)."""
+    rng = np.random.default_rng(77)
+    frames = []
+    for w in range(24):
+        kinds = [SHORT_KINDS[w % 5]] * 64
+        if w % 4 == 1:  # mixed layouts
+            kinds = [SHORT_KINDS[rng.integers(0, 5)] for _ in range(64)]
+        fr = [_short_frames(rng, k, 0, [rng.integers(40, 65)])[0] for k in kinds]
+        if w % 4 == 2:  # one long frame in the wave
+            fr[17] = bytes(synth.build_frames(rng, 1, synth.V4_UDP, 200)[0])
+        if w % 4 == 3:  # junk and truncated frames, skipped
+            fr[3] = bytes(rng.integers(0, 256, 30, dtype=np.uint8))
+            fr[9] = fr[9][:20]
+            fr[40] = b""
+        frames += fr
+    arena, off, ln = synth.pack_frames(frames)
+    for flags in (ALL, N.F_ACCEPT_V4 | N.F_ACCEPT_UDP, N.F_ACCEPT_V6 | N.F_ACCEPT_ICMP, ALL_EXT):
+        gpu_vs_oracle(ctx, arena, off, ln, flags, N.LAYER_L4)
+    # an unaligned frame in a short wave
+    off2 = off.copy()
+    off2[64 + 5] += 2
+    gpu_vs_oracle(ctx, arena, off2, ln, ALL, N.LAYER_L4)
+
+
+@pytest.mark.parametrize("tail_off", [24, 32, 50])
+def test_frame_past_arena_end_skipped(ctx, tail_off):
+    """A descriptor whose frame runs past arena_len (against the ABI's
+    precondition) is reported skipped and nothing is written past the end
+    (the field stores were unchecked)."""
+    rng = np.random.default_rng(tail_off)
+    frames = [bytes(f) for f in synth.build_frames(rng, 100, synth.V4_UDP, 64)]
+    arena, off, ln = synth.pack_frames(frames)
+    alen = len(arena) - 64 + tail_off  # the last frame keeps tail_off bytes inside
+    arena = arena[:alen]
+    padded = np.concatenate([arena, np.zeros(64, np.uint8)])  # zeros past the end, as the device reads
+    flags = N.F_ACCEPT_V4 | N.F_ACCEPT_UDP
+    want_meta, *_ = oracle_lib.parse_batch(padded, off, ln, flags, fields=False)
+    guard = torch.zeros(alen + 256, dtype=torch.uint8, device=DEV)
+    guard[:alen] = torch.from_numpy(arena).to(DEV)
+    b = packets.PacketBatch(guard[:alen], torch.from_numpy(off.view(np.int32)).to(DEV),
+                            torch.from_numpy(ln.view(np.int16)).to(DEV))
+    r = packets.parse(ctx, b, flags=flags)
+    meta = r.meta.cpu().numpy().view(np.uint32)
+    assert (meta == want_meta).all()
+    assert (meta[-1] & 0xFF) == 0  # the straddling frame parses (its tail reads as zeros)
+    st = packets.reconcile(ctx, b, r.meta, flags=flags, depth="l4")
+    want, want_st = oracle_lib.reconcile(padded, off, ln, meta, flags, N.LAYER_L4, arena_len=alen)
+    got = guard.cpu().numpy()
+    assert (got[alen:] == 0).all(), "written past arena_len"
+    assert (got[:alen] == want[:alen]).all()
+    assert (st.cpu().numpy() == want_st).all()
+    assert want_st[-1] == N.RECON_SKIPPED and (want_st[:-1] == N.RECON_OK).all()
