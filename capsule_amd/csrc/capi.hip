@@ -9,26 +9,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <dlfcn.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <new>
+#include <random>
 
 #include "capsule_gpu.h"
 #include "kernels.hpp"
 
-#ifndef CGPU_NAT64_EXT_EVENT  // 1: a nat64 call's completion event is its last kernel's stop event
-#define CGPU_NAT64_EXT_EVENT 1
-#endif
-// How a nat64 call orders itself behind the map's previous call: 1 waits
+// How a nat64 call orders itself behind the map's previous call: it waits
 // on the previous call's completion event unless both calls ran on the same
 // stream, told by stream id (hipStreamGetId: never reused, unlike a handle a
-// destroyed stream may hand to a new one); 0 always waits.  A wait on a
-// still-pending event of the same stream costs ~1.4 us per call on the
-// stream (measured).
-#ifndef CGPU_NAT64_SAME_STREAM_SKIP
-#define CGPU_NAT64_SAME_STREAM_SKIP 1
-#endif
+// destroyed stream may hand to a new one).  A wait on a still-pending event
+// of the same stream costs ~1.4 us per call on the stream (measured,
+// DESIGN.md §3.2).
 
 namespace {
 
@@ -681,10 +677,30 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
   pm->dev.rev = (uint32_t *)(p + o_rev);
   pm->dev.slots = (cgpu::PortSlot *)(p + o_slots);
   pm->dev.cap_mask = (uint32_t)(cap - 1);
+  // per-map random hash seeds (crafted keys cannot collide on purpose)
+  {
+    std::random_device rd;
+    pm->dev.seed_hash = rd();
+    pm->dev.seed_tag = rd();
+  }
   // Test hook: CGPU_TEST_NAT64_TAG_MASK=<hex> keeps only those bits of the
-  // claim tags, so distinct keys collide on them and the tail's repair runs.
+  // claim tags, so distinct keys collide on them and the tail's repair runs
+  // (every batch then takes the serial repair: slow, never wrong).  A value
+  // that is not a nonzero hex mask is ignored; an active hook says so once.
   pm->dev.tag_mask = 0xffffffffu;
-  if (const char *tm = getenv("CGPU_TEST_NAT64_TAG_MASK")) pm->dev.tag_mask = (uint32_t)strtoul(tm, nullptr, 16);
+  if (const char *tm = getenv("CGPU_TEST_NAT64_TAG_MASK")) {
+    char *end = nullptr;
+    const unsigned long v = strtoul(tm, &end, 16);
+    if (end != tm && *end == '\0' && (v & 0xffffffffu) != 0u) {
+      pm->dev.tag_mask = (uint32_t)v;
+      static bool said = false;
+      if (!said) {
+        said = true;
+        fprintf(stderr, "capsule_gpu: test hook CGPU_TEST_NAT64_TAG_MASK=%08x active (claim tags masked)\n",
+                pm->dev.tag_mask);
+      }
+    }
+  }
   if (hipEventCreateWithFlags(&pm->done, hipEventDisableTiming) != hipSuccess) {
     (void)hipFree(mem);
     delete pm;
@@ -821,23 +837,15 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   // handle (a destroyed stream's handle can come back for a new stream while
   // the old one's work is still pending).
   const unsigned long long sid = stream_id(stream);
-  if ((!CGPU_NAT64_SAME_STREAM_SKIP || sid == 0 || sid != pm->last_sid) &&
+  if ((sid == 0 || sid != pm->last_sid) &&
       hipStreamWaitEvent((hipStream_t)stream, pm->done, 0) != hipSuccess)
     return fail(CGPU_EIO);
   pm->last_sid = sid;
-#if CGPU_NAT64_EXT_EVENT
   // the completion event rides on the call's last kernel (no marker packet)
   hipError_t e = to4 ? cgpu::launch_nat64_6to4(a, (hipStream_t)stream, pm->done)
                      : cgpu::launch_nat64_4to6(a, (hipStream_t)stream, pm->done);
   if (e != hipSuccess) return hip_fail(e);
   if (to4) ++pm->calls;
-#else
-  hipError_t e = to4 ? cgpu::launch_nat64_6to4(a, (hipStream_t)stream, nullptr)
-                     : cgpu::launch_nat64_4to6(a, (hipStream_t)stream, nullptr);
-  if (e != hipSuccess) return hip_fail(e);
-  if (to4) ++pm->calls;
-  if (hipEventRecord(pm->done, (hipStream_t)stream) != hipSuccess) return fail(CGPU_EIO);
-#endif
   return ok();
 }
 

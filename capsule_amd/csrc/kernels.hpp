@@ -73,6 +73,7 @@ struct PortMapDev {
   uint32_t cap_mask;
   uint32_t tag_mask;  // claim-tag bits kept (all; a test build of the map keeps fewer:
                       // CGPU_TEST_NAT64_TAG_MASK, to exercise the tail's collision repair)
+  uint32_t seed_hash, seed_tag;  // per-map random seeds of key_hash / key_tag
 };
 
 struct Nat64Args {

@@ -47,16 +47,10 @@ namespace cgpu {
 namespace {
 
 constexpr uint32_t kBlock = 256;
-// cache policy bits of the frame-stream loads and stores (A/B knob; 0 =
-// default policy)
-#ifndef CGPU_NAT64_AUX
-#define CGPU_NAT64_AUX 0
-#endif
-constexpr int kAux = CGPU_NAT64_AUX;
-#ifndef CGPU_NAT64_WPE
-#define CGPU_NAT64_WPE 1
-#endif
-#define NAT64_OCC __attribute__((amdgpu_waves_per_eu(CGPU_NAT64_WPE)))
+// cache policy bits of the frame-stream loads and stores: the default
+// policy (nontemporal and sc1 variants were slower)
+constexpr int kAux = 0;
+#define NAT64_OCC __attribute__((amdgpu_waves_per_eu(1)))
 constexpr uint32_t kFG = 4u;                 // lanes per frame in the rewrite phase
 constexpr uint32_t kFJ = 16u / kFG;          // 16-B chunks per lane per 256-B pass
 constexpr uint32_t kNow = 4u;                // record info bit: rewrite in the fused kernel
@@ -83,8 +77,13 @@ __device__ __forceinline__ uint32_t rotl32(uint32_t x, int b) {
   return (x << b) | (x >> (32 - b));
 }
 
-__device__ __forceinline__ uint32_t key_hash(const uint32_t (&key)[5]) {
-  uint32_t h = 0x9e3779b9u;
+// Both hashes start from a per-map random seed (cgpu_portmap_create), so that
+// keys sharing a probe chain or a claim tag cannot be chosen from outside
+// (crafted collisions would send every such packet through the tail's serial
+// repair): a key word's difference reaches the state through a multiply mod
+// 2^32 of a seed-dependent value, so no difference cancels for every seed.
+__device__ __forceinline__ uint32_t key_hash(const uint32_t (&key)[5], uint32_t seed) {
+  uint32_t h = 0x9e3779b9u ^ seed;
 #pragma unroll
   for (int j = 0; j < 5; ++j) {
     h ^= key[j] * 0xcc9e2d51u;
@@ -101,8 +100,8 @@ __device__ __forceinline__ uint32_t key_hash(const uint32_t (&key)[5]) {
 // The claim tag: a second, independent hash of the key (a batch-local slot
 // whose tag differs holds another key; an equal tag is confirmed on the key
 // words).
-__device__ __forceinline__ uint32_t key_tag(const uint32_t (&key)[5]) {
-  uint32_t h = 0x2545f491u;
+__device__ __forceinline__ uint32_t key_tag(const uint32_t (&key)[5], uint32_t seed) {
+  uint32_t h = 0x2545f491u ^ seed;
 #pragma unroll
   for (int j = 0; j < 5; ++j) {
     h = (h ^ key[j]) * 0x9e3779b1u;
@@ -282,19 +281,12 @@ __device__ __forceinline__ void ipv4_header(const V6 &v, uint32_t len, uint32_t 
 // words were written by an earlier launch).  refs only ever go 0 -> (i + 1)
 // -> kPersist, and a claim's tag never changes, so a stale probe load at
 // worst leads to the CAS, which returns the coherent word.
-#ifndef CGPU_NAT64_LAZY_TAG
-#define CGPU_NAT64_LAZY_TAG 1
-#endif
 __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i,
                                                   const uint32_t (&key)[5], uint32_t h, u32x4 s0,
                                                   u32x4 s1, uint32_t &port) {
   port = 0xffffffffu;
-#if CGPU_NAT64_LAZY_TAG
   uint32_t tag = 0;  // computed when a slot is not a committed key (never in the steady state)
   bool have_tag = false;
-#else
-  const uint32_t tag = key_tag(key) & a.pm.tag_mask;
-#endif
   for (uint32_t probe = 0; probe <= a.pm.cap_mask; ++probe) {
     if (probe != 0u) {  // the first slot was loaded by the caller
       const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
@@ -303,12 +295,10 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
     }
     uint32_t *w = a.pm.slots[h].w;
     uint32_t ref = s0[0], stag = s0[1];
-#if CGPU_NAT64_LAZY_TAG
     if (!(ref & kPersist) && !have_tag) {
-      tag = key_tag(key) & a.pm.tag_mask;
+      tag = key_tag(key, a.pm.seed_tag) & a.pm.tag_mask;
       have_tag = true;
     }
-#endif
     if (ref == 0u) {
       const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long *>(w), 0ull,
                                                (unsigned long long)(i + 1u) |
@@ -347,7 +337,7 @@ __device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, uint32_t i, c
                                                uint32_t &port) {
   uint32_t key[5];
   make_key(v, key);
-  const uint32_t h = key_hash(key) & a.pm.cap_mask;
+  const uint32_t h = key_hash(key, a.pm.seed_hash) & a.pm.cap_mask;
   const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
   return probe_port_at(a, i, key, h, sp[0], sp[1], port);
 }
@@ -745,9 +735,7 @@ __device__ __forceinline__ void defer_append(const Nat64Args &a, uint32_t lane, 
   (void)i;
   const uint64_t dm = __ballot(flag);
   if (!dm) return;
-#ifndef CGPU_NAT64_ABL_NOFLAG  // timing ablation only (cold batches): no flag, the tail always runs
   if (lane == (uint32_t)__builtin_ctzll(dm)) a.pm.state[4u + a.par] = 1u;
-#endif
 }
 
 // The general path: one quad per frame (any alignment, any length); `i` is
@@ -769,12 +757,7 @@ __device__ __forceinline__ void quad_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   // assigned_port (main.rs:41-53): lane 0 of the quad probes the table
   uint32_t slot = kNoSlot, port = 0xffffffffu;
   if (d.valid && g == 0u && v.disp == CGPU_ACT) {
-#ifdef CGPU_NAT64_ABL_NOPROBE  // timing ablation only: every key committed, no table access
-    slot = 0u;
-    port = 1025u;
-#else
     slot = probe_port(a, d.i, v, port);
-#endif
   }
   slot = qbc<0>(slot);
   port = qbc<0>(port);
@@ -794,7 +777,6 @@ __device__ __forceinline__ void quad_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     a.status[d.i] = (uint8_t)v.st;
   }
   defer_append(a, lane, deferred && g == 0u, d.i);
-#ifndef CGPU_NAT64_ABL_NOREWRITE  // timing ablation only: classify + probe alone
   if (act) {  // a deferred frame is written with source port 0; the tail patches it
     FrameRec f;
     f.in_off = d.off;
@@ -809,7 +791,6 @@ __device__ __forceinline__ void quad_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     f.defer_i = deferred ? d.i : kNoSlot;
     rewrite_quad<true>(a, rs, ors, g, d, al16, f, X, E);
   }
-#endif
 }
 
 // ---- the rows path: F frames per wave ---------------------------------------
@@ -832,13 +813,7 @@ __device__ __forceinline__ void quad_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
 // layout), one output length for the wave (per-lane chunk masks computed
 // once).
 constexpr uint32_t kRowW = 20;  // LDS dwords per frame record
-#ifndef CGPU_NAT64_ROW_DLDS  // classification bytes from the rows via LDS (0: own loads)
-#define CGPU_NAT64_ROW_DLDS 1
-#endif
-#ifndef CGPU_NAT64_ROW_FRAMES
-#define CGPU_NAT64_ROW_FRAMES 32
-#endif
-constexpr uint32_t kRowFrames = CGPU_NAT64_ROW_FRAMES;  // frames per wave (32 or 64)
+constexpr uint32_t kRowFrames = 32;  // frames per wave (64: 152 us, 3 waves per SIMD)
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dppz(uint32_t v) {  // lanes without a source get 0
@@ -870,17 +845,10 @@ __device__ __forceinline__ void rows_build(const uint32_t (&D)[24], const uint32
   }
 }
 
-// Row-path cache policy of the frame loads and of the whole-row stores
-// (A/B knob: 2 = nontemporal; only the rows path writes whole lines per
-// instruction, so only it can use nontemporal stores without splitting them)
-#ifndef CGPU_NAT64_ROW_AUX
-#define CGPU_NAT64_ROW_AUX 0
-#endif
-#ifndef CGPU_NAT64_ROW_LD_AUX
-#define CGPU_NAT64_ROW_LD_AUX 0
-#endif
-constexpr int kRowAux = CGPU_NAT64_ROW_AUX;       // whole-row stores
-constexpr int kRowLdAux = CGPU_NAT64_ROW_LD_AUX;  // frame loads
+// Row-path cache policy of the frame loads and of the whole-row stores: the
+// default (nontemporal, aux 2, was slower: DESIGN.md §3.2)
+constexpr int kRowAux = 0;    // whole-row stores
+constexpr int kRowLdAux = 0;  // frame loads
 
 // B1: the payload of every round -- output chunks 4.. realigned in place
 // (X[r] becomes output chunk l of frame 4r + row) and their TCP sum, reduced
@@ -963,14 +931,6 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   if (__ballot(valid && ((off & 15u) != 0u || (o_off & 3u) != 0u || len > 256u))) return false;
   const uint32_t row = lane >> 4, l = lane & 15u;
   uint32_t D[24];
-#if !CGPU_NAT64_ROW_DLDS
-  // A1: this lane's own frame, input bytes 0..95, for the classification
-#pragma unroll
-  for (uint32_t m = 0; m < 6u; ++m) {
-    const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * m < len ? off + 16u * m : kNoRead), 0, kRowLdAux);
-    D[4 * m] = t[0]; D[4 * m + 1] = t[1]; D[4 * m + 2] = t[2]; D[4 * m + 3] = t[3];
-  }
-#endif
   // A2: the frames in rows, four whole frames per load instruction; in
   // flight while the headers are classified and the port map is probed
   u32x4 X[R];
@@ -980,7 +940,6 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     const uint32_t fo = __shfl(off, (int)f), fl = __shfl(len, (int)f);
     X[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(16u * l < fl ? fo + 16u * l : kNoRead), 0, kRowLdAux);
   }
-#if CGPU_NAT64_ROW_DLDS
   // A1: bytes 0..95 of every frame from its row, through wave-private LDS
   // (the record area, not yet in use) to the frame's own lane: no strided
   // per-lane loads of the header lines the rows have just fetched
@@ -994,7 +953,6 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     D[4 * m] = t[0]; D[4 * m + 1] = t[1]; D[4 * m + 2] = t[2]; D[4 * m + 3] = t[3];
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#endif
   uint32_t *rec = lds + (mine ? lane : 0u) * kRowW;
   // A3: the reference control flow; the first port-map slot of the key is
   // loaded now and examined after B1
@@ -1006,15 +964,13 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   const bool act0 = valid && v.disp == CGPU_ACT;
   uint32_t key[5];
   make_key(v, key);
-  const uint32_t h = key_hash(key) & a.pm.cap_mask;
+  const uint32_t h = key_hash(key, a.pm.seed_hash) & a.pm.cap_mask;
   u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
-#ifndef CGPU_NAT64_ABL_NOPROBE
   if (act0) {
     const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
     s0 = sp[0];
     s1 = sp[1];
   }
-#endif
   const uint32_t nl = len - 20u;  // meaningful for ACT frames
   if (mine) {
     rec[16] = act0 ? nl : 0u;
@@ -1029,12 +985,7 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   // A4: assigned_port (main.rs:41-53), the IPv4 header
   uint32_t slot = kNoSlot, port = 0xffffffffu;
   if (act0) {
-#ifdef CGPU_NAT64_ABL_NOPROBE
-    slot = 0u;
-    port = 1025u;
-#else
     slot = probe_port_at(a, i, key, h, s0, s1, port);
-#endif
   }
   if (v.disp == CGPU_ACT && slot == kNoSlot) {
     v.disp = CGPU_ABORT;
@@ -1072,14 +1023,10 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     *reinterpret_cast<u32x4 *>(rec + 16) =
         u32x4{act ? nl : 0u, payload + accA, ph | (k << 16), o_off};
     // a deferred frame's checksum (with port 0) and VLAN depth, for the tail
-#ifndef CGPU_NAT64_ABL_NOSTASHC0  // timing ablation only (steady state): without the stash store
     if (deferred) a.stash_c0[i] = ((~fold32(ph + swap16(fold32(payload + accA)))) & 0xffffu) | (k << 16);
-#endif
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#ifndef CGPU_NAT64_ABL_NOREWRITE
   rows_store(a, ors, X, lds, row, l);
-#endif
   return true;
 }
 
@@ -1203,10 +1150,7 @@ __device__ __forceinline__ void chunk_firsts(const Nat64Args &a, uint32_t c, boo
 // is issued before the first compare, so a workgroup waits on one chain of
 // dependent loads (pkt_slot -> slot) instead of U; the counts per wave go
 // through LDS (s_wc), one barrier for the U chunks.
-#ifndef CGPU_NAT64_ORDER_U
-#define CGPU_NAT64_ORDER_U 4
-#endif
-constexpr uint32_t kOrderU = CGPU_NAT64_ORDER_U;
+constexpr uint32_t kOrderU = 4;
 __device__ __forceinline__ void chunks_firsts(const Nat64Args &a, uint32_t c0, uint32_t stride,
                                               uint32_t nb, uint32_t *cnt, uint32_t *cmask,
                                               uint32_t *mism, const TailCtl &ctl,
@@ -1228,20 +1172,14 @@ __device__ __forceinline__ void chunks_firsts(const Nat64Args &a, uint32_t c0, u
       // the slot in two 16-B loads (w[2..7]: key words and first packet):
       // a gather costs per instruction and per line, not per byte
       const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[ps[j] & kSlotMask]);
-#ifdef CGPU_NAT64_ABL_NOSLOT  // timing ablation only: no slot read (wrong first packets)
-      w7[j] = (ps[j] & kClaimBit) ? i : kNoSlot;
-#else
       const u32x4 s1 = sp[1];
       w7[j] = s1[3];
-#ifndef CGPU_NAT64_ABL_NOVERIFY  // timing ablation only: tag joins trusted
       if (!(ps[j] & kClaimBit)) {
         const u32x4 s0 = sp[0];
         const u32x4 k = a.stash_key[i];
         bad[j] = k[0] != s0[2] || k[1] != s0[3] || k[2] != s1[0] || k[3] != s1[1] ||
                  (uint32_t)a.stash_port[i] != (s1[2] & 0xffffu);
       }
-#endif
-#endif
     }
   }
 #pragma unroll
@@ -1322,12 +1260,12 @@ __device__ void tail_repair(const Nat64Args &a, uint32_t nb, uint32_t nmism, con
       add_chunk(a.pm.slots[wrong].w[7]);  // the wrong slot's first packet so far
       const u32x4 sk = a.stash_key[m];
       const uint32_t key[5] = {sk[0], sk[1], sk[2], sk[3], (uint32_t)a.stash_port[m]};
-      uint32_t h = key_hash(key) & a.pm.cap_mask, res = kNoSlot;
+      uint32_t h = key_hash(key, a.pm.seed_hash) & a.pm.cap_mask, res = kNoSlot;
       for (uint32_t probe = 0; probe <= a.pm.cap_mask; ++probe, h = (h + 1u) & a.pm.cap_mask) {
         uint32_t *w = a.pm.slots[h].w;
         const uint32_t other[5] = {w[2], w[3], w[4], w[5], w[6] & 0xffffu};
         if (w[0] == 0u) {  // a new key after all: claim it
-          w[1] = key_tag(key) & a.pm.tag_mask;
+          w[1] = key_tag(key, a.pm.seed_tag) & a.pm.tag_mask;
           w[2] = key[0];
           w[3] = key[1];
           w[4] = key[2];
@@ -1460,10 +1398,6 @@ __device__ __forceinline__ void tail_scan(const Nat64Args &a, uint32_t nb, const
   }
 }
 
-#ifdef CGPU_NAT64_TAIL_CLOCK
-__device__ unsigned long long g_clk[2 * kOrderGrid];
-__device__ uint32_t g_clk_calls;
-#endif
 
 __device__ __forceinline__ uint32_t shard_size(uint32_t grid, uint32_t s) {
   return s < grid ? (grid - s + kShards - 1u) / kShards : 0u;
@@ -1477,26 +1411,12 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   // the previous call's flag, cleared only if set: in the steady state the
   // flag line is never written, so every workgroup's read of it can hit
   if (blockIdx.x == 0 && threadIdx.x == 0 && st[4u + (a.par ^ 1u)] != 0u) st[4u + (a.par ^ 1u)] = 0u;
-#ifndef CGPU_NAT64_ABL_NOFLAG
   if (st[4u + a.par] == 0u) return;  // nothing deferred: no new key
-#endif
   uint32_t *const cnt = a.chunks, *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
   uint32_t *const mism = a.chunks + 10u * nb;  // the tag collisions (packet indices)
   const TailCtl ctl = tail_ctl(a);
-#ifdef CGPU_NAT64_TAIL_CLOCK  // diagnosis only: the order launch's phases, printed for a few calls
-  // per workgroup (start, end of its chunks) in a device array, plain
-  // write-through stores: no atomics of their own
-  const unsigned long long ts = wall_clock64();
-#endif
   for (uint32_t c0 = blockIdx.x; c0 < nb; c0 += kOrderU * gridDim.x)
     chunks_firsts(a, c0, gridDim.x, nb, cnt, cmask, mism, ctl, s_wc);
-#ifdef CGPU_NAT64_TAIL_CLOCK
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(&g_clk[2 * blockIdx.x], ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&g_clk[2 * blockIdx.x + 1], (unsigned long long)wall_clock64(), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
-#endif
   __builtin_amdgcn_s_waitcnt(0);  // every storing wave drains before the arrival
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1513,32 +1433,8 @@ __global__ __launch_bounds__(kBlock) void nat64_tail_order(Nat64Args a, uint32_t
   if (!s_last) return;
   if (threadIdx.x == 0) s_nm = atomicCAS(&ctl.top[1], 0u, 0u);  // the collisions, read at the coherence point
   __syncthreads();
-#ifdef CGPU_NAT64_TAIL_CLOCK
-  const unsigned long long t2 = wall_clock64();
-#endif
   if (s_nm) tail_repair(a, nb, s_nm, mism, cnt, cmask, ctl);
   tail_scan(a, nb, cnt, cbase, ctl, s_part);
-#ifdef CGPU_NAT64_TAIL_CLOCK
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned long long t3 = wall_clock64();
-    unsigned long long s0 = ~0ull, s1 = 0, e1 = 0, dmax = 0, dsum = 0;
-    for (uint32_t b = 0; b < gridDim.x; ++b) {
-      const unsigned long long x = __hip_atomic_load(&g_clk[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long y = __hip_atomic_load(&g_clk[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s0 = x < s0 ? x : s0;
-      s1 = x > s1 ? x : s1;
-      e1 = y > e1 ? y : e1;
-      dmax = y - x > dmax ? y - x : dmax;
-      dsum += y - x;
-    }
-    const uint32_t call = g_clk_calls++;
-    if (call % 256u == 100u)
-      printf("order clock (10 ns): first start -> last chunk end %llu, last start %llu, workgroup mean %llu max %llu, "
-             "-> last arriver %llu, scan %llu, grid %u\n",
-             e1 - s0, s1 - s0, dsum / gridDim.x, dmax, t2 - e1, t3 - t2, gridDim.x);
-  }
-#endif
 }
 
 // One deferred packet: its key's port, the commit of a first packet, and
@@ -1594,9 +1490,6 @@ __device__ __forceinline__ void patch_packet(const Nat64Args &a, uint32_t i, uin
   // turn into a stray store)
   if (k > 2u || (uint64_t)o_off + 52u + 4u * k > a.out_arena_len) return;
   uint8_t *tcp = a.out_arena + o_off + 34u + 4u * k;  // the TCP header
-#ifdef CGPU_NAT64_ABL_NOPATCHSTORE  // timing ablation only: the frames are not patched
-  if (c == 0x12345u) tcp[0] = 0;
-#else
   if (!((o_off + 34u) & 1u)) {  // (packed 6to4 output: even) two 16-bit stores
     *reinterpret_cast<uint16_t *>(tcp) = (uint16_t)swap16(port);
     *reinterpret_cast<uint16_t *>(tcp + 16) = (uint16_t)swap16(c);
@@ -1606,13 +1499,10 @@ __device__ __forceinline__ void patch_packet(const Nat64Args &a, uint32_t i, uin
     tcp[16] = (uint8_t)(c >> 8);
     tcp[17] = (uint8_t)c;
   }
-#endif
 }
 
 __global__ __launch_bounds__(kBlock) void nat64_tail_patch(Nat64Args a, uint32_t nb) {
-#ifndef CGPU_NAT64_ABL_NOFLAG
   if (a.pm.state[4u + a.par] == 0u) return;  // nothing deferred: no new key
-#endif
   const uint32_t *const cbase = a.chunks + nb, *const cmask = a.chunks + 2u * nb;
   const uint32_t port_base = tail_ctl(a).top[2];
   for (uint32_t c = blockIdx.x; c < nb; c += gridDim.x) {
@@ -1939,10 +1829,7 @@ __device__ __forceinline__ void quad_4to6(const Nat64Args &a, rsrc_t rs, rsrc_t 
   rewrite_quad<false>(a, rs, ors, g, d, al16, f, X, E);
 }
 
-#ifndef CGPU_NAT64_4TO6_WPE
-#define CGPU_NAT64_4TO6_WPE 4
-#endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CGPU_NAT64_4TO6_WPE)))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
 void nat64_4to6_fused(Nat64Args a) {
   __shared__ uint32_t lds[kBlock / 64][kRowFrames * kRowW6];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -1950,10 +1837,7 @@ void nat64_4to6_fused(Nat64Args a) {
   if (base >= a.n) return;  // wave-uniform
   const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
   const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
-#ifndef CGPU_NAT64_4TO6_ROWS  // A/B knob: 0 = every wave takes the quad path
-#define CGPU_NAT64_4TO6_ROWS 1
-#endif
-  if (CGPU_NAT64_4TO6_ROWS && rows_4to6(a, rs, ors, base, lane, lds[wave])) return;
+  if (rows_4to6(a, rs, ors, base, lane, lds[wave])) return;
   for (uint32_t q = 0; q < kRowFrames / 16u; ++q) quad_4to6(a, rs, ors, base + 16u * q + lane / 4u, lane);
 }
 
@@ -1998,10 +1882,6 @@ hipError_t launch_nat64_6to4(const Nat64Args &a, hipStream_t s, hipEvent_t done)
   const uint32_t nb = nat64_num_blocks(a.n);
   const uint32_t fpb = (kBlock / 64u) * kRowFrames;  // fused: kRowFrames frames per wave
   const uint32_t nbf = (a.n + fpb - 1) / fpb;
-#ifdef CGPU_NAT64_ABL_NOTAIL  // timing ablation only (steady state): what the tail launches cost
-  hipExtLaunchKernelGGL(nat64_6to4_fused, dim3(nbf), dim3(kBlock), 0, s, nullptr, done, 0, a);
-  return hipGetLastError();
-#endif
   hipLaunchKernelGGL(nat64_6to4_fused, dim3(nbf), dim3(kBlock), 0, s, a);
   // the tail: the order of the new keys, then their frames' ports; in the
   // steady state (no new key) both grids return at once

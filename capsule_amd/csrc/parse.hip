@@ -38,46 +38,19 @@ namespace cgpu {
 
 namespace {
 
-#ifndef CGPU_PARSE_BLOCK
-#define CGPU_PARSE_BLOCK 256
-#endif
-constexpr uint32_t kBlock = CGPU_PARSE_BLOCK;
+constexpr uint32_t kBlock = 256;
 constexpr int kWin = 24;        // packet-relative window dwords (96 B)
 constexpr uint32_t kQEnd = 88;  // normalized window bytes valid after a QinQ shift
 constexpr uint32_t kNoRead = 0xffffff00u;  // > any arena_len the ABI accepts
 constexpr uint32_t kSlotPieces = 2;  // longest tail (256-B pieces) summed in slots
-#ifndef CGPU_SLOT_IT
-#define CGPU_SLOT_IT 4
-#endif
-constexpr uint32_t kSlotIt = CGPU_SLOT_IT;  // slots per 16-lane row and round (loads in flight)
-#ifndef CGPU_PARSE_ROWS
-#define CGPU_PARSE_ROWS 1
-#endif
-#ifndef CGPU_PARSE_LINE0_MIN  // 0: off
-#define CGPU_PARSE_LINE0_MIN 512
-#endif
-#ifndef CGPU_PARSE_ROWS_MEAN_MAX  // largest mean slot (arena bytes / packet) given the rows variant
-#define CGPU_PARSE_ROWS_MEAN_MAX 2200
-#endif
-#ifndef CGPU_PARSE_ROW_MAX
-#define CGPU_PARSE_ROW_MAX 512
-#endif
-constexpr uint32_t kRowMaxLen = CGPU_PARSE_ROW_MAX;  // the rows path: frames up to 2 pieces
-// reconcile: 1 rewrites a frame's first 64 B whole, 0 stores the fields
-// alone.  Measured (round 4, 1 Mi frames): field stores 41.1 us at 64 B and
-// 125.6 us IMIX, whole 64 B 51.6 / 146.3 us (WRITE_SIZE 64 / 119 MB against
-// 90 / 177 MB): the 64-B sector is written back either way, and the whole
-// rewrite only adds store traffic.
-#ifndef CGPU_RECON_WHOLE
-#define CGPU_RECON_WHOLE 0
-#endif
-// reconcile: frames 16-B aligned and at least 64 B long get their first 64 B
-// stored four lanes per frame, so that one store instruction writes whole
-// 64-B pieces of 16 frames (full sectors in 64-B slots) instead of each lane
-// storing 2-B fields into its own frame's sector (0: field stores only).
-#ifndef CGPU_RECON_COAL
-#define CGPU_RECON_COAL 1
-#endif
+constexpr uint32_t kSlotIt = 4;  // slots per 16-lane row and round (loads in flight)
+constexpr uint32_t kRowMaxLen = 512;  // the rows path: frames up to 2 pieces
+// the rows variant of the checksum configs: batches whose mean slot (arena
+// bytes per packet) is 128..kRowsMeanMax B (long frames, but not jumbo ones)
+constexpr uint32_t kRowsMeanMax = 2200;
+// frames of at least this many bytes sum the rest of their window's line
+// early (below: bound by HBM bytes rather than by strided requests)
+constexpr uint32_t kLine0Min = 512;
 
 __device__ __forceinline__ uint32_t sel3(uint32_t k, uint32_t a, uint32_t b, uint32_t c) {
   return k == 0u ? a : (k == 1u ? b : c);
@@ -258,13 +231,7 @@ __device__ __forceinline__ void rows_prologue(rsrc_t rs, uint32_t off, uint32_t 
 // window + tail path, no line is read twice: a long frame's last line is
 // often the next frame's first, which the tail pass fetched again after
 // the window pass had let it go.
-#ifndef CGPU_PARSE_STREAM
-#define CGPU_PARSE_STREAM 1
-#endif
-#ifndef CGPU_STREAM_U
-#define CGPU_STREAM_U 3
-#endif
-constexpr uint32_t kStreamU = CGPU_STREAM_U;  // 1 KiB loads in flight per lane and step
+constexpr uint32_t kStreamU = 3;  // 1 KiB loads in flight per lane and step
 constexpr uint32_t kStreamMax = 32768;  // span bytes per wave: 2048 chunks, one bitmap word per lane
 
 
@@ -447,33 +414,23 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
   bool rows = false;     // the rows path (above): window and frame sum from rows
   bool stream = false;   // the stream path (above): frame sums from the wave's span
   uint32_t s_all = 0, st_base = 0, st_span = 0;
-#if CGPU_PARSE_ROWS
   if (ROWS) {
     const bool bad = valid && ((off & 15u) != 0u || (uint64_t)off + len + 16u > (uint64_t)a.arena_len);
     const uint64_t vm = __ballot(valid);
     rows = vm && !__ballot(bad) &&
            2u * (uint32_t)__popcll(__ballot(valid && len >= 128u)) >= (uint32_t)__popcll(vm);
-#if CGPU_PARSE_STREAM
     // waves of mostly long frames keep the rows (as fast, fewer VALU per
     // byte); the stream takes mixed waves (IMIX), whose short frames would
     // leave 12 of a row's 16 lanes idle
     stream = !rows && stream_wave(off, len, valid, threadIdx.x & 63u, a.arena_len, st_base, st_span);
-#endif
   }
-#endif
   const bool slow = (off & 3u) != 0u || (uint64_t)off + 96u > (uint64_t)a.arena_len;
-#if CGPU_PARSE_ROWS
   constexpr uint32_t kPathLds = kRowLds > kStreamLds ? kRowLds : kStreamLds;
   __shared__ uint32_t rlds[ROWS ? kBlock / 64 : 1][ROWS ? kPathLds : 1];
-#endif
   if (ROWS && rows) {
-#if CGPU_PARSE_ROWS
     rows_prologue(rs, valid ? off : 0u, valid ? len : 0u, threadIdx.x & 63u, rlds[threadIdx.x >> 6], P, s_all);
-#endif
   } else if (ROWS && stream) {
-#if CGPU_PARSE_ROWS && CGPU_PARSE_STREAM
     stream_prologue(rs, st_base, st_span, off, len, threadIdx.x & 63u, rlds[threadIdx.x >> 6], P, s_all);
-#endif
   } else if (__ballot(slow)) {
     load_window_general(rs, a.arena_len, off, len, P);
   } else {
@@ -514,16 +471,15 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
         P[4 * c + 2] = v[2];
         P[4 * c + 3] = v[3];
       }
-#if CGPU_PARSE_LINE0_MIN
       // A long frame's checksum tail would start at (off + 64) & ~15 and
       // fetch the rest of this 128-B line again, after the 4 MB L2 has
       // evicted it: the lane sums those chunks now, with the window in
       // flight (at most 4, all inside the frame), and the tail starts on the
-      // next line.  Frames of CGPU_PARSE_LINE0_MIN bytes and more only, where
+      // next line.  Frames of kLine0Min bytes and more only, where
       // the kernel is bound by HBM bytes rather than by strided requests.
       if (L4C) {
         const uint32_t tb = (off + 64u) & ~15u, lb = (tb + 127u) & ~127u;
-        const uint32_t nc = wlim == 64u && len >= CGPU_PARSE_LINE0_MIN && lb < off + len ? (lb - tb) >> 4 : 0u;
+        const uint32_t nc = wlim == 64u && len >= kLine0Min && lb < off + len ? (lb - tb) >> 4 : 0u;
         if (__ballot(nc != 0u)) {
           u32x4 v[4];
 #pragma unroll
@@ -534,7 +490,6 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
           l0_adv = 16u * (nc < 4u ? nc : 4u);
         }
       }
-#endif
     } else if (V4U) {
       // no frame of the wave reaches byte 64: in the IPv4/UDP variant these
       // words are only read by the checksum sums, which skip or mask them
@@ -545,7 +500,6 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
       for (int j = 16; j < kWin; ++j) P[j] = 0u;
     }
   }
-#if CGPU_PARSE_ROWS && CGPU_RECON_COAL
   if constexpr (RECON && ROWS) {
     // the window's first 64 B, for the coalesced store at the end (the
     // wave's LDS is free once the prologue has handed the windows over)
@@ -556,7 +510,6 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
     for (int m = 0; m < 4; ++m)
       *reinterpret_cast<u32x4 *>(pl + 4 * m) = u32x4{P[4 * m], P[4 * m + 1], P[4 * m + 2], P[4 * m + 3]};
   }
-#endif
 
   // --- Ethernet: VLAN marker at bytes 12-13 (ethernet.rs:164-181) ---------
   const uint32_t marker = be16_lo(P[3]);
@@ -913,7 +866,6 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
     const uint32_t t_to = off + len;
     const uint32_t lane = threadIdx.x & 63u, grp = lane >> 4, l16 = lane & 15u;
     uint32_t tail = 0;
-#if CGPU_PARSE_LINE0_MIN
     // the window line's rest (see the window loads): summed early, or now
     // (waves that took the general window loader)
     if (l0_adv != 0u && has_tail) {
@@ -922,7 +874,7 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
     }
     {
       const uint32_t lb = (t_b + 127u) & ~127u;
-      const uint32_t nc = has_tail && l0_adv == 0u && len >= CGPU_PARSE_LINE0_MIN && lb < t_to ? (lb - t_b) >> 4 : 0u;
+      const uint32_t nc = has_tail && l0_adv == 0u && len >= kLine0Min && lb < t_to ? (lb - t_b) >> 4 : 0u;
       if (__ballot(nc != 0u)) {
         u32x4 v[4];
 #pragma unroll
@@ -933,7 +885,6 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
         t_b += 16u * (nc < 4u ? nc : 4u);
       }
     }
-#endif
     const uint32_t pieces = has_tail ? (t_to - t_b + 255u) >> 8 : 0u;  // 256-B pieces
     const bool slot_tail = has_tail && pieces <= kSlotPieces;
     // every chunk any tail needs lies inside the arena: branch-free loads
@@ -1107,7 +1058,6 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
     }
     uint8_t *f = a.wr_arena + off;
     bool stored = false;  // the fields below byte 64 went out with the whole 64 B
-#if CGPU_RECON_COAL
     // Whole waves only (every lane holds a packet: each lane stores chunks of
     // other lanes' frames).  A frame goes out this way if it is reconciled,
     // 16-B aligned and at least 64 B long; its first 64 B are the window P
@@ -1136,11 +1086,9 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
         const uint32_t foff = (uint32_t)__shfl((int)off, (int)fr);
         const bool fw = (wm >> fr) & 1ull;
         u32x4 v;
-#if CGPU_PARSE_ROWS
         if (ROWS)
           v = *reinterpret_cast<const u32x4 *>(&rlds[threadIdx.x >> 6][16u * fr + 4u * c]);
         else
-#endif
           v = __builtin_amdgcn_raw_buffer_load_b128(ws, (int)(fw ? foff + 16u * c : kNoRead), 0, 0);
 #pragma unroll
         for (uint32_t q = 0; q < 4u; ++q) {
@@ -1154,32 +1102,7 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
       }
       stored = whole;
     }
-#endif
     if (rec) {
-#if CGPU_RECON_WHOLE
-      // A dword-aligned frame of 64 B or more gets its first 64 bytes back
-      // whole from its own lane (four 16-B stores into its sector).
-      if (!stored && (off & 3u) == 0u && len >= 64u) {
-        uint32_t W[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) W[j] = P[j];
-#pragma unroll
-        for (uint32_t q = 0; q < 4u; ++q) {
-          if (q >= nf) break;
-          const uint32_t pos = fp[q], v = swap16(fv[q]);
-#pragma unroll
-          for (int j = 0; j < 16; ++j)
-            if ((pos >> 2) == (uint32_t)j)
-              W[j] = (pos & 2u) ? ((W[j] & 0xffffu) | (v << 16)) : ((W[j] & 0xffff0000u) | v);
-        }
-        const rsrc_t ws = make_rsrc(a.wr_arena, a.arena_len);
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{W[4 * c], W[4 * c + 1], W[4 * c + 2], W[4 * c + 3]}, ws,
-                                                 (int)(off + 16u * c), 0, 0);
-        stored = true;
-      }
-#endif
       // the fields not yet stored (all of them, or those past byte 64: IPv6
       // behind tags, its TCP checksum)
 #pragma unroll
@@ -1400,15 +1323,13 @@ __device__ __forceinline__ bool recon_short(const ParseArgs &a) {
 
 // The reconcile kernels: the same body with their own occupancy targets
 // (workgroups of 256 per CU).  The window variant (short frames: every
-// frame's sector is read and written back in place) runs at 6: 45.95
-// against 50.5 us at 8 for 1 Mi x 64 B, A/B on one box (fewer waves
-// contending for the same read-modify-write traffic); the rows variant
-// (IMIX) keeps 8 (128.5 against 126.2 us at 6).
-#ifndef CGPU_RECON_WPE_WIN
-#define CGPU_RECON_WPE_WIN 6
-#endif
+// frame's sector is read and written back in place) runs at 6; a round-4
+// A/B against 8 (45.95 against 50.5 us at 1 Mi x 64 B) was within that
+// launch's run-to-run spread (44.9-50.0 us for 6 on one box), and with the
+// short path 6 and 8 time the same (32.6 us, round 5).  The rows variant
+// (IMIX) keeps 8: 126.2 us against 128.5 us at 6 (round 4, one box).
 template <bool L4C, bool EXT, bool V4U>
-__global__ __launch_bounds__(kBlock, CGPU_RECON_WPE_WIN) void recon_kernel(ParseArgs a) {
+__global__ __launch_bounds__(kBlock, 6) void recon_kernel(ParseArgs a) {
   if constexpr (L4C) {
     if (recon_short<EXT, V4U>(a)) return;
   }
@@ -1426,7 +1347,7 @@ hipError_t launch_t(const ParseArgs &a, hipStream_t s) {
   // when the batch's mean slot (arena bytes per packet) is 128..2200 B: long
   // frames, but not jumbo ones; each wave still decides by its own frames.
   const uint64_t mean = (uint64_t)a.arena_len / a.n;
-  if (L4C && CGPU_PARSE_ROWS && mean >= 128u && mean <= CGPU_PARSE_ROWS_MEAN_MAX)
+  if (L4C && mean >= 128u && mean <= kRowsMeanMax)
     hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, V4U, true>), dim3(grid), dim3(kBlock), 0, s, a);
   else
     hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, V4U, false>), dim3(grid), dim3(kBlock), 0, s, a);
@@ -1456,7 +1377,7 @@ template <bool L4C, bool EXT, bool V4U>
 hipError_t launch_recon_t(const ParseArgs &a, hipStream_t s) {
   const uint32_t grid = (a.n + kBlock - 1) / kBlock;
   const uint64_t mean = (uint64_t)a.arena_len / a.n;
-  if (L4C && CGPU_PARSE_ROWS && mean >= 128u && mean <= CGPU_PARSE_ROWS_MEAN_MAX)
+  if (L4C && mean >= 128u && mean <= kRowsMeanMax)
     hipLaunchKernelGGL((recon_rows_kernel<L4C, EXT, V4U>), dim3(grid), dim3(kBlock), 0, s, a);
   else
     hipLaunchKernelGGL((recon_kernel<L4C, EXT, V4U>), dim3(grid), dim3(kBlock), 0, s, a);
