@@ -14,7 +14,7 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ.get("CAPSULE_GPU_LIB", _HERE / "libcapsule_gpu.so"))
 
 # ---- constants (include/capsule_gpu.h) ------------------------------------
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 OK, EINVAL, ENOMEM, ENODEV, EIO, ENOSPC = 0, -22, -12, -19, -5, -28
 
@@ -131,7 +131,7 @@ EXPORTS = [
     "cgpu_portmap_size", "cgpu_nat64_6to4", "cgpu_nat64_4to6", "cgpu_group_by", "cgpu_last_error", "cgpu_strerror",
     "cgpu_pkt_status_str", "cgpu_abi_version", "cgpu_host_register", "cgpu_host_unregister",
     "cgpu_parse_mbufs", "cgpu_set_ip", "cgpu_nat64_mbufs", "cgpu_parse_frames",
-    "cgpu_nat64_frames", "cgpu_portmap_reset", "cgpu_reconcile",
+    "cgpu_nat64_frames", "cgpu_portmap_reset", "cgpu_reconcile", "cgpu_reconcile_frames",
 ]
 
 _lib = None
@@ -195,6 +195,8 @@ def lib():
     L.cgpu_set_ip.argtypes = [vp, vp, ctypes.c_uint64, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp]
     L.cgpu_reconcile.restype = i32
     L.cgpu_reconcile.argtypes = [vp, vp, ctypes.c_uint64, vp, vp, vp, u32, u32, u32, vp, vp]
+    L.cgpu_reconcile_frames.restype = i32
+    L.cgpu_reconcile_frames.argtypes = [vp, vp, vp, vp, u32, u32, u32, vp]
     if L.cgpu_abi_version() != ABI_VERSION:
         raise RuntimeError("capsule_amd: libcapsule_gpu.so ABI version mismatch")
     _lib = L

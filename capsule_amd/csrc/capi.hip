@@ -15,6 +15,7 @@
 
 #include <new>
 #include <random>
+#include <vector>
 
 #include "capsule_gpu.h"
 #include "kernels.hpp"
@@ -1096,6 +1097,101 @@ int cgpu_reconcile(cgpu_ctx *ctx, uint8_t *arena, uint64_t arena_len, const uint
   a.rstatus = status;
   hipError_t e = cgpu::launch_reconcile(a, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e);
+  return ok();
+}
+
+// cgpu_reconcile over frames in registered host memory: each region's
+// frames are one arena window (its base the lowest frame address rounded
+// down to 256 B, so a frame's alignment within the window is its own), and
+// the reconcile kernel runs on the device's mapping of that window.
+int cgpu_reconcile_frames(cgpu_ctx *ctx, uint8_t *const *frames, const uint16_t *len,
+                          const uint32_t *meta, uint32_t n, uint32_t flags, uint32_t depth,
+                          uint8_t *status) {
+  if (!ctx || n > CGPU_MAX_BATCH) return fail(CGPU_EINVAL);
+  if (depth != CGPU_LAYER_L2 && depth != CGPU_LAYER_L3 && depth != CGPU_LAYER_L4)
+    return fail(CGPU_EINVAL);
+  if (n == 0) return ok();
+  if (!frames || !len || !meta || ctx->nreg == 0) return fail(CGPU_EINVAL);
+  // every frame inside one registered region (checked before anything runs)
+  std::vector<uint8_t> region(n);
+  uint64_t lo[cgpu::kMaxRegions], hi[cgpu::kMaxRegions];
+  uint32_t cnt[cgpu::kMaxRegions] = {};
+  uint32_t last = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t a = (uint64_t)(uintptr_t)frames[i], e = a + len[i];
+    auto inside = [&](uint32_t r) {
+      const cgpu::HostRegion &g = ctx->reg[r];
+      return a >= g.host_base && e <= g.host_base + g.bytes && (a != 0 || len[i] == 0);
+    };
+    uint32_t r = last;
+    if (!inside(r)) {
+      for (r = 0; r < ctx->nreg && !inside(r); ++r) {
+      }
+      if (r == ctx->nreg) return fail(CGPU_EINVAL);
+      last = r;
+    }
+    region[i] = (uint8_t)r;
+    if (cnt[r]++ == 0) {
+      lo[r] = a;
+      hi[r] = e;
+    } else {
+      lo[r] = a < lo[r] ? a : lo[r];
+      hi[r] = e > hi[r] ? e : hi[r];
+    }
+  }
+  for (uint32_t r = 0; r < ctx->nreg; ++r) {
+    if (!cnt[r]) continue;
+    lo[r] &= ~(uint64_t)255u;
+    if (lo[r] < ctx->reg[r].host_base) lo[r] = ctx->reg[r].host_base;
+    if (hi[r] - lo[r] > 0xffff0000ull) return fail(CGPU_EINVAL);
+  }
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
+  // staging: off u32 | len u16 | meta u32 | status u8, per region's frames
+  const size_t o_off = 0, o_len = align_up(4ull * n, 256), o_meta = o_len + align_up(2ull * n, 256);
+  const size_t o_st = o_meta + align_up(4ull * n, 256), o_end = o_st + align_up(n, 256);
+  if (int e = grow(&ctx->h_desc, &ctx->d_desc, &ctx->desc_cap, o_end)) return fail(e);
+  uint8_t *D = ctx->d_desc, *H = ctx->h_desc;
+  hipStream_t s = ctx->stream;
+  if ((flags & (CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6)) == 0) flags |= CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6;
+  if ((flags & (CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP | CGPU_F_ACCEPT_ICMP)) == 0)
+    flags |= CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP;
+  for (uint32_t r = 0; r < ctx->nreg; ++r) {
+    if (!cnt[r]) continue;
+    uint32_t *ho = (uint32_t *)(H + o_off), *hm = (uint32_t *)(H + o_meta);
+    uint16_t *hl = (uint16_t *)(H + o_len);
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      if (region[i] != r) continue;
+      ho[m] = (uint32_t)((uint64_t)(uintptr_t)frames[i] - lo[r]);
+      hl[m] = len[i];
+      hm[m] = meta[i];
+      ++m;
+    }
+    if (hipMemcpyAsync(D, H, o_st, hipMemcpyHostToDevice, s) != hipSuccess) return fail(CGPU_EIO);
+    uint8_t *win = (uint8_t *)(uintptr_t)(ctx->reg[r].dev_base + (lo[r] - ctx->reg[r].host_base));
+    cgpu::ParseArgs a{};
+    a.arena = win;
+    a.arena_len = (uint32_t)(hi[r] - lo[r]);
+    a.off = (const uint32_t *)(D + o_off);
+    a.len = (const uint16_t *)(D + o_len);
+    a.n = m;
+    a.accept = flags & (CGPU_F_ACCEPT_ALL | CGPU_F_ACCEPT_ICMP | CGPU_F_V6_EXT);
+    a.wr_arena = win;
+    a.meta_in = (const uint32_t *)(D + o_meta);
+    a.depth = depth;
+    a.rstatus = D + o_st;
+    hipError_t e = cgpu::launch_reconcile(a, s);
+    if (e != hipSuccess) return hip_fail(e);
+    if (hipMemcpyAsync(H + o_st, D + o_st, m, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return fail(CGPU_EIO);
+    if (status) {
+      uint32_t q = 0;
+      for (uint32_t i = 0; i < n; ++i)
+        if (region[i] == r) status[i] = H[o_st + q++];
+    }
+  }
   return ok();
 }
 

@@ -848,7 +848,7 @@ __device__ __forceinline__ void rows_build(const uint32_t (&D)[24], const uint32
 // Row-path cache policy of the frame loads and of the whole-row stores: the
 // default (nontemporal, aux 2, was slower: DESIGN.md §3.2)
 constexpr int kRowAux = 0;    // whole-row stores
-constexpr int kRowLdAux = 0;  // frame loads
+constexpr int kRowLdAux = 2;  // frame loads: nontemporal (whole lines per instruction)
 
 // B1: the payload of every round -- output chunks 4.. realigned in place
 // (X[r] becomes output chunk l of frame 4r + row) and their TCP sum, reduced

@@ -407,6 +407,26 @@ def reconcile(ctx, batch, meta, flags=None, depth="l4", stream=None, status=None
     return status
 
 
+def reconcile_frames(ctx, addrs, lens, meta, flags=None, depth="l4"):
+    """`reconcile_all` over a burst handed over as host (data_address,
+    data_len) pairs in registered host memory (cgpu_reconcile_frames), in
+    place; `meta` the host parse words of those bytes (e.g. from
+    `parse_frames`).  Returns the status per frame (RECON_OK / _SKIPPED)."""
+    if flags is None:
+        flags = parse_flags()
+    addrs = np.ascontiguousarray(addrs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    meta = np.ascontiguousarray(meta, dtype=np.uint32)
+    n = len(addrs)
+    if len(lens) != n or len(meta) != n:
+        raise ValueError("addrs, lens and meta must have one entry per frame")
+    st = np.zeros(n, np.uint8)
+    rc = N.lib().cgpu_reconcile_frames(ctx.handle, addrs.ctypes.data, lens.ctypes.data,
+                                       meta.ctypes.data, n, flags, _DEPTH[depth], st.ctypes.data)
+    N.check(rc, "cgpu_reconcile_frames")
+    return st
+
+
 class ReconcileLauncher:
     """A `reconcile` call with prebuilt ctypes arguments (bench loops)."""
 

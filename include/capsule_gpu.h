@@ -39,8 +39,10 @@ extern "C" {
  *      data_off + data_len > buf_len are rejected (CGPU_EINVAL); the mbuf
  *      and frame-pair entry points also check that every byte a frame may
  *      be rewritten into lies in a registered region.
- *   4  cgpu_reconcile (Packet::reconcile_all over a parsed batch).          */
-#define CGPU_ABI_VERSION 4
+ *   4  cgpu_reconcile (Packet::reconcile_all over a parsed batch).
+ *   5  cgpu_reconcile_frames (the same over frames in registered host
+ *      memory, in place: the mbuf seam of a reconcile combinator).          */
+#define CGPU_ABI_VERSION 5
 
 /* ---- call-level return codes (negative errno style) -------------------- */
 #define CGPU_OK 0
@@ -464,6 +466,23 @@ enum cgpu_recon_status { CGPU_RECON_OK = 0, CGPU_RECON_SKIPPED = 1 };
 int cgpu_reconcile(cgpu_ctx *ctx, uint8_t *arena, uint64_t arena_len, const uint32_t *off,
                    const uint16_t *len, const uint32_t *meta, uint32_t n, uint32_t flags,
                    uint32_t depth, uint8_t *status, void *stream);
+
+/* The same over a burst as the RX path hands it over: frames[i] =
+ * Mbuf::data_address(0), len[i] = data_len (mbuf.rs:196-205), in memory
+ * registered with cgpu_host_register (a mempool's memzone), reconciled in
+ * place through the device's mapping of that memory: no staging copy, the
+ * device reads each frame once and writes the rewritten fields back.
+ * meta[i]: the words a parse of these bytes returned (host array, e.g. from
+ * cgpu_parse_frames), flags / depth / status (host, optional) as
+ * cgpu_reconcile.  Every frame must lie wholly inside one registered region,
+ * and a region's frames of one call within 4 GiB - 64 KiB of each other;
+ * otherwise CGPU_EINVAL and nothing is written.  Synchronous; uses the
+ * context's stream (one call at a time per context).  Replaces
+ * packet.reconcile_all() (packets/mod.rs:297-300) inside a pipeline closure
+ * over a burst whose typed packets came from the device parse.              */
+int cgpu_reconcile_frames(cgpu_ctx *ctx, uint8_t *const *frames, const uint16_t *len,
+                          const uint32_t *meta, uint32_t n, uint32_t flags, uint32_t depth,
+                          uint8_t *status);
 
 /* ---- errors -------------------------------------------------------------- */
 int cgpu_last_error(void);

@@ -96,6 +96,9 @@ static int (*const p_set_ip)(cgpu_ctx *, uint8_t *, uint64_t, const uint32_t *,
 static int (*const p_reconcile)(cgpu_ctx *, uint8_t *, uint64_t, const uint32_t *,
                                 const uint16_t *, const uint32_t *, uint32_t, uint32_t, uint32_t,
                                 uint8_t *, void *) = cgpu_reconcile;
+static int (*const p_reconcile_frames)(cgpu_ctx *, uint8_t *const *, const uint16_t *,
+                                       const uint32_t *, uint32_t, uint32_t, uint32_t,
+                                       uint8_t *) = cgpu_reconcile_frames;
 static int (*const p_last_error)(void) = cgpu_last_error;
 static const char *(*const p_strerror)(int) = cgpu_strerror;
 static const char *(*const p_pkt_status_str)(int) = cgpu_pkt_status_str;
@@ -110,7 +113,7 @@ static const any_fn entry_points[] = {
     (any_fn)p_set_ip,         (any_fn)p_last_error,       (any_fn)p_strerror,
     (any_fn)p_parse_frames,   (any_fn)p_nat64_frames,
     (any_fn)p_pkt_status_str, (any_fn)p_abi_version,    (any_fn)p_portmap_reset,
-    (any_fn)p_reconcile,
+    (any_fn)p_reconcile,      (any_fn)p_reconcile_frames,
 };
 
 int main(void) {

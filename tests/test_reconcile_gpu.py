@@ -301,3 +301,60 @@ def test_frame_past_arena_end_skipped(ctx, tail_off):
     assert (got[:alen] == want[:alen]).all()
     assert (st.cpu().numpy() == want_st).all()
     assert want_st[-1] == N.RECON_SKIPPED and (want_st[:-1] == N.RECON_OK).all()
+
+
+# ---- cgpu_reconcile_frames: the mbuf seam (frames in registered host memory) ----
+
+@pytest.mark.parametrize("kind", ["imix", "fuzz", "short"])
+def test_reconcile_frames_in_registered_mempool(ctx, kind):
+    """reconcile_all over (data_address, data_len) pairs in a registered
+    mempool, in place through the device mapping: every byte of the pool
+    against the oracle on the same frames (including the mbuf headers and
+    headroom between them, which must stay untouched)."""
+    if kind == "imix":
+        a, o, l = synth.imix(3000, seed=31, vlan_frac=0.2)
+    elif kind == "fuzz":
+        a, o, l = synth.fuzz(2000, seed=32)
+    else:
+        rng = np.random.default_rng(33)
+        frames = [f for k in SHORT_KINDS for f in _short_frames(rng, k, 0, rng.integers(40, 65, 100))]
+        a, o, l = synth.pack_frames(frames)
+    mem, mbufs = synth.mbuf_pool(a, o, l)
+    addrs, lens = synth.mbuf_frames(mem, mbufs)
+    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    try:
+        meta = packets.parse_frames(ctx, addrs, lens, ALL, N.INGRESS_ZERO_COPY)[0]
+        assert (meta == oracle_lib.parse_batch(a, o, l, ALL)[0]).all()
+        # stale the fields in the pool itself (frame offsets within the pool)
+        base = mem.ctypes.data
+        fo = (addrs - np.uint64(base)).astype(np.uint32)
+        synth.stale_fields(mem, fo, lens, meta, seed=9)
+        want, want_st = oracle_lib.reconcile(mem, fo, lens, meta, ALL, N.LAYER_L4)
+        st = packets.reconcile_frames(ctx, addrs, lens, meta, ALL, "l4")
+    finally:
+        reg.close()
+    assert (st == want_st).all()
+    bad = np.nonzero(mem != want)[0]
+    assert len(bad) == 0, f"{len(bad)} pool bytes differ, first at {bad[:4]}"
+    assert (want_st == N.RECON_OK).sum() > len(addrs) // 2
+
+
+def test_reconcile_frames_rejects_unregistered(ctx):
+    """A frame outside every registered region fails the call before any
+    frame is written."""
+    a, o, l = synth.imix(256, seed=5)
+    mem, mbufs = synth.mbuf_pool(a, o, l)
+    addrs, lens = synth.mbuf_frames(mem, mbufs)
+    other = np.zeros(4096, np.uint8)
+    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    try:
+        meta = packets.parse_frames(ctx, addrs, lens, ALL, N.INGRESS_ZERO_COPY)[0]
+        synth.stale_fields(mem, (addrs - np.uint64(mem.ctypes.data)).astype(np.uint32), lens, meta)
+        before = mem.copy()
+        bad = addrs.copy()
+        bad[77] = np.uint64(other.ctypes.data)
+        with pytest.raises(N.CgpuError):
+            packets.reconcile_frames(ctx, bad, lens, meta, ALL)
+        assert (mem == before).all()
+    finally:
+        reg.close()
