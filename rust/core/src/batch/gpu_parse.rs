@@ -12,68 +12,73 @@
 //! inside a `filter_map` closure.  Not compiled in this repository (no Rust
 //! toolchain).
 use super::{Batch, Disposition};
-use crate::gpu::{status_str, GpuContext, GpuDisposition, GpuNat64, Parsed, ParsedBurst};
-use crate::packets::{Internal, Packet};
+use crate::gpu::{status_str, GpuContext, GpuDisposition, GpuNat64, GpuTyped, Parsed, ParsedBurst};
 use crate::Mbuf;
-use anyhow::{anyhow, Result};
+use anyhow::anyhow;
 use std::collections::VecDeque;
 
-/// An mbuf with its device parse results (meta, checksums, flow hash).
-pub struct GpuParsed {
-    mbuf: Mbuf,
-    pub parsed: Parsed, // #[derive(Clone, Copy)]: meta / csum / hash of this packet
-}
-
-impl Packet for GpuParsed {
-    type Envelope = Mbuf;
-    fn envelope(&self) -> &Mbuf { &self.mbuf }
-    fn envelope_mut(&mut self) -> &mut Mbuf { &mut self.mbuf }
-    fn offset(&self) -> usize { 0 }
-    fn header_len(&self) -> usize { 0 }
-    unsafe fn clone(&self, internal: Internal) -> Self {
-        GpuParsed { mbuf: Packet::clone(&self.mbuf, internal), parsed: self.parsed }
-    }
-    fn try_parse(_: Mbuf, _: Internal) -> Result<Self> {
-        Err(anyhow!("GpuParsed is produced by GpuParse only."))
-    }
-    fn try_push(_: Mbuf, _: Internal) -> Result<Self> {
-        Err(anyhow!("GpuParsed is produced by GpuParse only."))
-    }
-    fn deparse(self) -> Mbuf { self.mbuf }
-}
-
-pub struct GpuParse<B: Batch<Item = Mbuf>> {
+/// `batch.map(|p| p.parse::<Ethernet>()?.parse::<Ipv4>()?.parse::<Udp4>())`
+/// as one device call per burst: yields the reference's own typed packet
+/// (`Udp4`, `Tcp6`, `Ipv4`, `Ethernet`, ...) built from the device parse, so
+/// the closures downstream (`filter_map(|udp: Udp4| ...)`, `udp.src_port()`,
+/// `udp.flow()`, `udp.reconcile_all()`) run unchanged and nothing is parsed
+/// again on the CPU.  The device results the reference would compute on the
+/// CPU afterwards (the flow hash, the checksum verification) reach an
+/// optional `inspect_parsed` closure next to each packet.
+pub struct GpuParse<B: Batch<Item = Mbuf>, T: GpuTyped> {
     batch: B,
     ctx: GpuContext,
     flags: u32,
     out: ParsedBurst,
-    ready: VecDeque<Disposition<GpuParsed>>,
+    ready: VecDeque<Disposition<T>>,
+    on_parsed: Option<Box<dyn FnMut(&T, &Parsed)>>,
 }
 
-impl<B: Batch<Item = Mbuf>> GpuParse<B> {
-    pub fn new(batch: B, ctx: GpuContext, flags: u32) -> Self {
-        GpuParse { batch, ctx, flags, out: ParsedBurst::default(), ready: VecDeque::new() }
+impl<B: Batch<Item = Mbuf>, T: GpuTyped> GpuParse<B, T> {
+    /// The typed chain's accept set, with the checksums verified and the flow
+    /// hash computed (g::CGPU_F_CSUM_IP | CSUM_L4 | FLOW_HASH).
+    pub fn new(batch: B, ctx: GpuContext) -> Self {
+        use capsule_gpu_ffi as g;
+        let flags = T::ACCEPT | g::CGPU_F_CSUM_IP | g::CGPU_F_CSUM_L4 | g::CGPU_F_FLOW_HASH;
+        Self::with_flags(batch, ctx, flags)
+    }
+
+    /// Explicit flags (T::ACCEPT is always added): e.g. no checksums.
+    pub fn with_flags(batch: B, ctx: GpuContext, flags: u32) -> Self {
+        GpuParse { batch, ctx, flags: flags | T::ACCEPT, out: ParsedBurst::default(),
+                   ready: VecDeque::new(), on_parsed: None }
+    }
+
+    /// Called with each Act packet and its device results as it is yielded.
+    pub fn inspect_parsed<F: FnMut(&T, &Parsed) + 'static>(mut self, f: F) -> Self {
+        self.on_parsed = Some(Box::new(f));
+        self
     }
 }
 
-impl<B: Batch<Item = Mbuf>> Batch for GpuParse<B> {
-    type Item = GpuParsed;
+/// Drains the upstream burst: Act mbufs in one vector (in order), the other
+/// dispositions kept in their places (None marks an Act slot).
+fn drain_burst<B: Batch>(batch: &mut B) -> (Vec<Option<Disposition<B::Item>>>, Vec<B::Item>) {
+    let mut slots = Vec::new();
+    let mut act = Vec::new();
+    while let Some(d) = batch.next() {
+        match d {
+            Disposition::Act(p) => {
+                slots.push(None);
+                act.push(p);
+            }
+            other => slots.push(Some(other)),
+        }
+    }
+    (slots, act)
+}
+
+impl<B: Batch<Item = Mbuf>, T: GpuTyped> Batch for GpuParse<B, T> {
+    type Item = T;
 
     fn replenish(&mut self) {
         self.batch.replenish();
-        // the upstream burst: Act packets go to the device in one call, the
-        // other dispositions keep their place (None marks an Act slot)
-        let mut slots: Vec<Option<Disposition<Mbuf>>> = Vec::new();
-        let mut act: Vec<Mbuf> = Vec::new();
-        while let Some(d) = self.batch.next() {
-            match d {
-                Disposition::Act(m) => {
-                    slots.push(None);
-                    act.push(m);
-                }
-                other => slots.push(Some(other)),
-            }
-        }
+        let (slots, act) = drain_burst(&mut self.batch);
         let (act, rc) = if act.is_empty() { (act, Ok(())) } else {
             self.ctx.parse_burst(act, self.flags, &mut self.out)
         };
@@ -90,10 +95,14 @@ impl<B: Batch<Item = Mbuf>> Batch for GpuParse<B> {
                         Err(e) => Disposition::Abort(anyhow!("GPU parse failed: {}", e)),
                         Ok(()) => {
                             let parsed = self.out.get(i);
-                            if parsed.meta & 0xff == 0 {
-                                Disposition::Act(GpuParsed { mbuf, parsed })
-                            } else {
-                                Disposition::Abort(anyhow!("{}", status_str(parsed.meta & 0xff)))
+                            match T::from_gpu(mbuf, &parsed) {
+                                Ok(pkt) => {
+                                    if let Some(f) = self.on_parsed.as_mut() {
+                                        f(&pkt, &parsed);
+                                    }
+                                    Disposition::Act(pkt)
+                                }
+                                Err(e) => Disposition::Abort(e),
                             }
                         }
                     }
@@ -107,6 +116,77 @@ impl<B: Batch<Item = Mbuf>> Batch for GpuParse<B> {
         self.ready.pop_front()
     }
 }
+
+/// `batch.map(|mut p| { p.reconcile_all(); Ok(p) })` (packets/mod.rs:297-300)
+/// over a burst of typed packets in one device call (cgpu_reconcile_frames):
+/// the burst's frames are reconciled in place in the registered mempool,
+/// from the packets' own layer (their type) outward, and come back Act in
+/// upstream order.  Typically after closures that rewrote ports or
+/// addresses: `GpuParse::<_, Udp4>::new(..).map(|mut u| { u.set_dst_port(53);
+/// Ok(u) }).gpu_reconcile(ctx)`.
+pub struct GpuReconcile<B: Batch<Item = T>, T: GpuTyped> {
+    batch: B,
+    ctx: GpuContext,
+    ready: VecDeque<Disposition<T>>,
+}
+
+impl<B: Batch<Item = T>, T: GpuTyped> GpuReconcile<B, T> {
+    pub fn new(batch: B, ctx: GpuContext) -> Self {
+        GpuReconcile { batch, ctx, ready: VecDeque::new() }
+    }
+}
+
+impl<B: Batch<Item = T>, T: GpuTyped> Batch for GpuReconcile<B, T> {
+    type Item = T;
+
+    fn replenish(&mut self) {
+        self.batch.replenish();
+        let (slots, act) = drain_burst(&mut self.batch);
+        let rc = if act.is_empty() { Ok(Vec::new()) } else { self.ctx.reconcile_typed(&act) };
+        let mut act = act.into_iter().enumerate();
+        for s in slots {
+            let d = match s {
+                Some(d) => d,
+                None => {
+                    let (i, pkt) = act.next().expect("one packet per Act slot");
+                    match &rc {
+                        Err(e) => Disposition::Abort(anyhow!("GPU reconcile failed: {}", e)),
+                        // every typed packet reconciles (reconcile_all is
+                        // infallible); skipped would mean a frame that
+                        // shrank below its own headers
+                        Ok(done) if done[i] => Disposition::Act(pkt),
+                        Ok(_) => Disposition::Abort(anyhow!("reconcile skipped: the frame no longer holds its headers.")),
+                    }
+                }
+            };
+            self.ready.push_back(d);
+        }
+    }
+
+    fn next(&mut self) -> Option<Disposition<Self::Item>> {
+        self.ready.pop_front()
+    }
+}
+
+/// The combinators as methods, like the reference's `Batch` provided methods
+/// (batch/mod.rs:137-387).
+pub trait GpuBatchExt: Batch + Sized {
+    fn gpu_parse<T: GpuTyped>(self, ctx: GpuContext) -> GpuParse<Self, T>
+    where
+        Self: Batch<Item = Mbuf>,
+    {
+        GpuParse::new(self, ctx)
+    }
+
+    fn gpu_reconcile(self, ctx: GpuContext) -> GpuReconcile<Self, Self::Item>
+    where
+        Self::Item: GpuTyped,
+    {
+        GpuReconcile::new(self, ctx)
+    }
+}
+
+impl<B: Batch> GpuBatchExt for B {}
 
 
 /// `install_6to4` / `install_4to6` (examples/nat64/main.rs:152-165) as one

@@ -13,6 +13,9 @@
 //! bytes for one call and never frees or keeps an mbuf.
 use crate::Mbuf;
 use crate::ffi;
+use crate::packets::ip::v4::Ipv4;
+use crate::packets::ip::v6::Ipv6;
+use crate::packets::{Ethernet, Packet, Tcp, Udp};
 use capsule_gpu_ffi as g;
 use std::ffi::{c_void, CStr};
 use std::net::IpAddr;
@@ -74,6 +77,22 @@ impl GpuContext {
         (mbufs, rc)
     }
 
+    /// `reconcile_all` (packets/mod.rs:297-300) in place over typed packets
+    /// whose frames lie in a registered mempool (cgpu_reconcile_frames): each
+    /// packet's layers come from its type, so nothing is parsed again.
+    /// Returns one flag per packet: reconciled (true) or skipped.
+    pub fn reconcile_typed<T: GpuTyped>(&mut self, pkts: &[T]) -> anyhow::Result<Vec<bool>> {
+        let frames: Vec<*mut u8> = pkts.iter().map(|p| unsafe { p.mbuf().data_address(0) }).collect();
+        let lens: Vec<u16> = pkts.iter().map(|p| p.mbuf().data_len() as u16).collect();
+        let meta: Vec<u32> = pkts.iter().map(|p| p.gpu_meta()).collect();
+        let mut st = vec![0u8; pkts.len()];
+        check(unsafe {
+            g::cgpu_reconcile_frames(self.0, frames.as_ptr(), lens.as_ptr(), meta.as_ptr(),
+                                     pkts.len() as u32, T::ACCEPT, T::DEPTH, st.as_mut_ptr())
+        })?;
+        Ok(st.iter().map(|&s| s == g::cgpu_recon_status::CGPU_RECON_OK as u8).collect())
+    }
+
     /// The same burst as (data_address, data_len) pairs: the core reads the
     /// mbuf headers it has just written, the device reads only the frames.
     pub fn parse_burst_frames(&mut self, mbufs: &[Mbuf], flags: u32, out: &mut ParsedBurst)
@@ -108,6 +127,26 @@ pub struct Parsed {
 impl Parsed {
     pub fn status(&self) -> u32 {
         self.meta & 0xff
+    }
+    /// g::CGPU_L3_*: the IP layer the parse found (0 none).
+    pub fn l3(&self) -> u32 {
+        (self.meta >> 16) & 3
+    }
+    /// g::CGPU_L4_*: the L4 layer the parse found (0 none).
+    pub fn l4(&self) -> u32 {
+        (self.meta >> 18) & 3
+    }
+    /// The flow hash of `Udp::flow` / `Tcp::flow` (udp.rs:151-159,
+    /// tcp.rs:409-417) under DESIGN.md §4's convention.
+    pub fn flow_hash(&self) -> u64 {
+        self.hash
+    }
+    /// The IPv4 header and L4 checksums as stored equal the recomputed ones.
+    pub fn ip_csum_ok(&self) -> bool {
+        self.meta & g::CGPU_META_IP_CSUM_OK != 0
+    }
+    pub fn l4_csum_ok(&self) -> bool {
+        self.meta & g::CGPU_META_L4_CSUM_OK != 0
     }
     pub fn is_ok(&self) -> bool {
         self.status() == g::cgpu_pkt_status::CGPU_PKT_OK
@@ -291,3 +330,149 @@ impl Drop for GpuNat64 {
         unsafe { g::cgpu_portmap_destroy(self.pm) }
     }
 }
+
+/// The layer a per-packet status names (2 Ethernet, 3 IP, 4 L4): a typed
+/// chain of depth d fails only on statuses of layers <= d, as
+/// `p.parse::<Ethernet>()?.parse::<Ipv4>()?` never looks at L4.
+fn status_layer(status: u32) -> u32 {
+    use g::cgpu_pkt_status::*;
+    match status {
+        CGPU_PKT_ETH_BAD_OFFSET | CGPU_PKT_ETH_OUT_OF_BUFFER => 2,
+        CGPU_PKT_NOT_IPV4 | CGPU_PKT_NOT_IPV6 | CGPU_PKT_NOT_IP | CGPU_PKT_L3_BAD_OFFSET
+        | CGPU_PKT_L3_OUT_OF_BUFFER => 3,
+        _ => 4,
+    }
+}
+
+/// The reference's typed packets, built from the device parse instead of
+/// `parse::<Ethernet>()?.parse::<Ipv4>()?.parse::<Udp4>()?`.  Each layer is
+/// made by the `pub(crate)` constructor `from_device(envelope, offset)` that
+/// rust/README.md adds to the layer's own file: the struct the reference's
+/// `try_parse` returns (ethernet.rs:279-300, ip/v4.rs:427-442, ip/v6/mod.rs:
+/// 274-289, udp.rs:287-302, tcp.rs:558-573), with the header pointer at the
+/// envelope's payload offset, without `read_data`'s bounds check and the
+/// `ensure!`s: the device's status byte says they passed.
+pub trait GpuTyped: Packet + Sized {
+    /// The accept set of the parse (g::CGPU_F_ACCEPT_*): the typed chain.
+    const ACCEPT: u32;
+    /// g::CGPU_LAYER_*: the layer the chain ends at.
+    const DEPTH: u32;
+
+    /// The typed packet, or the reference's error of the first layer of the
+    /// chain that failed (its message as `try_parse` words it).
+    fn from_gpu(mbuf: Mbuf, parsed: &Parsed) -> anyhow::Result<Self> {
+        let st = parsed.status();
+        if st != g::cgpu_pkt_status::CGPU_PKT_OK && status_layer(st) <= Self::DEPTH {
+            return Err(anyhow::anyhow!("{}", status_str(st)));
+        }
+        // the layers the type names, as the parse found them (a packet of
+        // another kind fails like try_parse's ensure! does)
+        Self::check_kind(parsed)?;
+        Ok(unsafe { Self::build(mbuf) })
+    }
+
+    /// The kind check of the typed chain against the parse's layers.
+    fn check_kind(parsed: &Parsed) -> anyhow::Result<()>;
+
+    /// The typed packet over `mbuf`, every layer's header at its envelope's
+    /// payload offset.
+    ///
+    /// # Safety
+    ///
+    /// The device parse of these bytes found exactly these layers, in bounds.
+    unsafe fn build(mbuf: Mbuf) -> Self;
+
+    /// The meta word that describes this packet's layers to the reconcile
+    /// kernel (status OK, Ethernet header length and VLAN bits, L3, L4).
+    fn gpu_meta(&self) -> u32;
+}
+
+fn eth_meta(eth: &Ethernet) -> u32 {
+    let hl = eth.header_len() as u32;
+    let vlan = match hl {
+        18 => g::CGPU_META_DOT1Q,
+        22 => g::CGPU_META_QINQ,
+        _ => 0,
+    };
+    (hl << 8) | vlan
+}
+
+fn kind_err(want: u32, got: u32, msg: &str) -> anyhow::Result<()> {
+    if want == got {
+        Ok(())
+    } else {
+        Err(anyhow::anyhow!("{}", msg))
+    }
+}
+
+impl GpuTyped for Ethernet {
+    const ACCEPT: u32 = 0;
+    const DEPTH: u32 = g::CGPU_LAYER_L2;
+    fn check_kind(_: &Parsed) -> anyhow::Result<()> {
+        Ok(())
+    }
+    unsafe fn build(mbuf: Mbuf) -> Self {
+        Ethernet::from_device(mbuf, 0)
+    }
+    fn gpu_meta(&self) -> u32 {
+        eth_meta(self)
+    }
+}
+
+impl GpuTyped for Ipv4 {
+    const ACCEPT: u32 = g::CGPU_F_ACCEPT_V4;
+    const DEPTH: u32 = g::CGPU_LAYER_L3;
+    fn check_kind(p: &Parsed) -> anyhow::Result<()> {
+        kind_err(g::CGPU_L3_IPV4, p.l3(), "not an IPv4 packet.")
+    }
+    unsafe fn build(mbuf: Mbuf) -> Self {
+        let eth = <Ethernet as GpuTyped>::build(mbuf);
+        let at = eth.payload_offset();
+        Ipv4::from_device(eth, at)
+    }
+    fn gpu_meta(&self) -> u32 {
+        eth_meta(self.envelope()) | (g::CGPU_L3_IPV4 << 16)
+    }
+}
+
+impl GpuTyped for Ipv6 {
+    const ACCEPT: u32 = g::CGPU_F_ACCEPT_V6;
+    const DEPTH: u32 = g::CGPU_LAYER_L3;
+    fn check_kind(p: &Parsed) -> anyhow::Result<()> {
+        kind_err(g::CGPU_L3_IPV6, p.l3(), "not an IPv6 packet.")
+    }
+    unsafe fn build(mbuf: Mbuf) -> Self {
+        let eth = <Ethernet as GpuTyped>::build(mbuf);
+        let at = eth.payload_offset();
+        Ipv6::from_device(eth, at)
+    }
+    fn gpu_meta(&self) -> u32 {
+        eth_meta(self.envelope()) | (g::CGPU_L3_IPV6 << 16)
+    }
+}
+
+/// Udp4 / Udp6 / Tcp4 / Tcp6 (udp.rs:358-361, tcp.rs:625-628).
+macro_rules! gpu_l4 {
+    ($ty:ident, $ip:ident, $l4:expr, $acc:expr, $msg:expr) => {
+        impl GpuTyped for $ty<$ip> {
+            const ACCEPT: u32 = <$ip as GpuTyped>::ACCEPT | $acc;
+            const DEPTH: u32 = g::CGPU_LAYER_L4;
+            fn check_kind(p: &Parsed) -> anyhow::Result<()> {
+                <$ip as GpuTyped>::check_kind(p)?;
+                kind_err($l4, p.l4(), $msg)
+            }
+            unsafe fn build(mbuf: Mbuf) -> Self {
+                let ip = <$ip as GpuTyped>::build(mbuf);
+                let at = ip.payload_offset();
+                $ty::from_device(ip, at)
+            }
+            fn gpu_meta(&self) -> u32 {
+                self.envelope().gpu_meta() | ($l4 << 18)
+            }
+        }
+    };
+}
+gpu_l4!(Udp, Ipv4, g::CGPU_L4_UDP, g::CGPU_F_ACCEPT_UDP, "not a UDP packet.");
+gpu_l4!(Udp, Ipv6, g::CGPU_L4_UDP, g::CGPU_F_ACCEPT_UDP, "not a UDP packet.");
+gpu_l4!(Tcp, Ipv4, g::CGPU_L4_TCP, g::CGPU_F_ACCEPT_TCP, "not a TCP packet.");
+gpu_l4!(Tcp, Ipv6, g::CGPU_L4_TCP, g::CGPU_F_ACCEPT_TCP, "not a TCP packet.");
