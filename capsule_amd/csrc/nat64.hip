@@ -895,7 +895,22 @@ __device__ __forceinline__ void rows_payload(u32x4 (&X)[kRowFrames / 4], uint32_
 
 // B2: row j writes frame 4r + j in one store instruction (whole lines):
 // lanes 0-3 the chunks built in A, lanes 4.. the realigned payload; lane 3
-// patches the TCP checksum into its chunk.
+// patches the TCP checksum into its chunk.  The chunk of lane l of frame
+// 4r + row, as stored.
+__device__ __forceinline__ u32x4 rows_chunk(const u32x4 (&X)[kRowFrames / 4], const uint32_t *fr, uint32_t r,
+                                            uint32_t l, const u32x4 &meta) {
+  const u32x4 hc = *reinterpret_cast<const u32x4 *>(fr + 4u * (l & 3u));
+  u32x4 o = l < 4u ? hc : X[r];
+  if (l == 3u) {
+    const uint32_t fk = meta[2] >> 16, fph = meta[2] & 0xffffu;
+    const uint32_t tcp_c = (~fold32(fph + swap16(fold32(meta[1])))) & 0xffffu;
+#pragma unroll
+    for (uint32_t t = 0; t < 4u; ++t)
+      if (t == fk) o[t] |= swap16(tcp_c) << 16;
+  }
+  return o;
+}
+
 __device__ __forceinline__ void rows_store(const Nat64Args &a, rsrc_t ors, const u32x4 (&X)[kRowFrames / 4],
                                            const uint32_t *lds, uint32_t row, uint32_t l) {
 #pragma unroll
@@ -904,15 +919,7 @@ __device__ __forceinline__ void rows_store(const Nat64Args &a, rsrc_t ors, const
     const u32x4 meta = *reinterpret_cast<const u32x4 *>(fr + 16);
     const uint32_t fnl = meta[0];
     if (!__ballot(fnl != 0u)) continue;  // no frame of this round is finished here
-    const u32x4 hc = *reinterpret_cast<const u32x4 *>(fr + 4u * (l & 3u));
-    u32x4 o = l < 4u ? hc : X[r];
-    if (l == 3u) {
-      const uint32_t fk = meta[2] >> 16, fph = meta[2] & 0xffffu;
-      const uint32_t tcp_c = (~fold32(fph + swap16(fold32(meta[1])))) & 0xffffu;
-#pragma unroll
-      for (uint32_t t = 0; t < 4u; ++t)
-        if (t == fk) o[t] |= swap16(tcp_c) << 16;
-    }
+    const u32x4 o = rows_chunk(X, fr, r, l, meta);
     if (fnl != 0u) {
       const uint32_t b0 = 16u * l;
       if (b0 + 16u <= fnl) __builtin_amdgcn_raw_buffer_store_b128(o, ors, (int)(meta[3] + b0), 0, kRowAux);
@@ -921,8 +928,66 @@ __device__ __forceinline__ void rows_store(const Nat64Args &a, rsrc_t ors, const
   }
 }
 
+// B2 for a wave whose 32 frames are all Act and packed back to back in the
+// output (out_off[f + 1] = out_off[f] + new length, lengths multiples of 4:
+// the bench's egress image, a TX ring): each half of the wave (16 frames,
+// at most 3,776 B) is assembled in wave-private LDS by the rows and then
+// stored linearly, 1 KiB per instruction.  The 128-B lines that lie wholly
+// inside the half's span are stored nontemporal (whole lines: the output
+// stream then does not push the port map's probe lines out of the L2, as
+// whole-slot nontemporal stores did for 4to6); the half's two boundary lines,
+// which the neighbouring half or wave also writes, keep the default policy.
+constexpr uint32_t kStageDw = 16u * 236u / 4u;  // one half-wave's output, dwords
+constexpr int kStageNT = 2;
+
+__device__ __forceinline__ void rows_store_staged(rsrc_t ors, const u32x4 (&X)[kRowFrames / 4], const uint32_t *lds,
+                                                  uint32_t *stage, uint32_t row, uint32_t l, uint32_t lane) {
+#pragma unroll
+  for (uint32_t h = 0; h < 2u; ++h) {
+    const uint32_t S = lds[16u * h * kRowW + 19u];  // the half's first frame's output offset
+    const uint32_t *lr = lds + (16u * h + 15u) * kRowW;
+    const uint32_t E = lr[19] + lr[16];  // its last frame's end
+#pragma unroll
+    for (uint32_t rr = 0; rr < 4u; ++rr) {
+      const uint32_t r = 4u * h + rr;
+      const uint32_t *fr = lds + (4u * r + row) * kRowW;
+      const u32x4 meta = *reinterpret_cast<const u32x4 *>(fr + 16);
+      const u32x4 o = rows_chunk(X, fr, r, l, meta);
+      const uint32_t d0 = (meta[3] - S) / 4u + 4u * l;  // the chunk's first dword in the stage
+#pragma unroll
+      for (uint32_t t = 0; t < 4u; ++t)
+        if (16u * l + 4u * t < meta[0]) stage[d0 + t] = o[t];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const uint32_t A = S & ~15u, nch = (E - A + 15u) >> 4;
+    for (uint32_t c = lane; c < nch; c += 64u) {
+      const uint32_t g = A + 16u * c;
+      u32x4 v;
+#pragma unroll
+      for (uint32_t t = 0; t < 4u; ++t) {
+        const uint32_t b = g + 4u * t;
+        v[t] = b >= S && b < E ? stage[(b - S) / 4u] : 0u;
+      }
+      if (g >= S && g + 16u <= E) {
+        const uint32_t line = g & ~127u;
+        if (line >= S && line + 128u <= E)
+          __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)g, 0, kStageNT);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)g, 0, 0);
+      } else {
+#pragma unroll
+        for (uint32_t t = 0; t < 4u; ++t) {
+          const uint32_t b = g + 4u * t;
+          if (b >= S && b < E) __builtin_amdgcn_raw_buffer_store_b32(v[t], ors, (int)b, 0, 0);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+}
+
 __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t ors, uint32_t base,
-                                          uint32_t lane, uint32_t *lds) {
+                                          uint32_t lane, uint32_t *lds, uint32_t *stage) {
   constexpr uint32_t R = kRowFrames / 4u;  // rounds
   const uint32_t i = base + lane;
   const bool mine = lane < kRowFrames;
@@ -1030,18 +1095,24 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     if (deferred) a.stash_c0[i] = ((~fold32(ph + swap16(fold32(payload + accA)))) & 0xffffu) | (k << 16);
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  rows_store(a, ors, X, lds, row, l);
+  // the staged store: every frame of the wave Act, the outputs tiling one
+  // span in frame order (dword lengths)
+  const uint32_t nxt = __shfl_down(o_off, 1);
+  const bool untiled = mine && (!act || (nl & 3u) != 0u || (lane + 1u < kRowFrames && nxt != o_off + nl));
+  if (!__ballot(untiled)) rows_store_staged(ors, X, lds, stage, row, l, lane);
+  else rows_store(a, ors, X, lds, row, l);
   return true;
 }
 
 __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a) {
   __shared__ uint32_t lds[kBlock / 64][kRowFrames * (kRowW > 24u ? kRowW : 24u)];
+  __shared__ uint32_t stage[kBlock / 64][kStageDw];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t base = (blockIdx.x * (kBlock / 64u) + wave) * kRowFrames;
   if (base >= a.n) return;  // wave-uniform
   const rsrc_t rs = make_rsrc(a.arena, a.arena_len);
   const rsrc_t ors = make_rsrc(a.out_arena, a.out_arena_len);
-  if (rows_6to4(a, rs, ors, base, lane, lds[wave])) return;
+  if (rows_6to4(a, rs, ors, base, lane, lds[wave], stage[wave])) return;
   // the general path: rounds of 16 frames, a quad per frame
   for (uint32_t q = 0; q < kRowFrames / 16u; ++q) quad_6to4(a, rs, ors, base + 16u * q + lane / 4u, lane);
 }
