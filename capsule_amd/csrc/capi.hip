@@ -110,6 +110,7 @@ struct cgpu_portmap {
   cgpu::u32x4 *stash_key = nullptr;
   uint16_t *stash_port = nullptr;
   uint32_t *stash_c0 = nullptr;
+  uint8_t *wave_flag = nullptr;
   uint32_t scratch_n = 0;
   uint32_t calls = 0;  // 6to4 calls: parity of the deferred-list counter
   // recorded on the stream of every call that uses the map: calls on one
@@ -794,13 +795,15 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
     const size_t o_key = o_chunks + align_up(cgpu::nat64_chunk_bytes(in->n), 256);
     const size_t o_port = o_key + align_up(16ull * in->n, 256);
     const size_t o_c0 = o_port + align_up(2ull * in->n, 256);
-    const size_t o_end = o_c0 + align_up(4ull * in->n, 256);
+    const size_t o_wf = o_c0 + align_up(4ull * in->n, 256);
+    const size_t o_end = o_wf + align_up(in->n / 32u + 1u, 256);
     if (hipMalloc(&m, o_end) != hipSuccess) return fail(CGPU_ENOMEM);
     pm->pkt_slot = (uint32_t *)m;
     pm->chunks = (uint32_t *)((uint8_t *)m + o_chunks);
     pm->stash_key = (cgpu::u32x4 *)((uint8_t *)m + o_key);
     pm->stash_port = (uint16_t *)((uint8_t *)m + o_port);
     pm->stash_c0 = (uint32_t *)((uint8_t *)m + o_c0);
+    pm->wave_flag = (uint8_t *)m + o_wf;
     // the tail's control lines start at zero; its last workgroup leaves them so
     if (hipMemsetAsync((uint8_t *)pm->chunks + cgpu::nat64_ctl_offset(in->n), 0,
                        cgpu::nat64_chunk_bytes(in->n) - cgpu::nat64_ctl_offset(in->n),
@@ -824,6 +827,7 @@ static int nat64_call(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, const cgpu_batc
   a.disposition = disposition;
   a.status = status;
   a.pkt_slot = pm->pkt_slot;
+  a.wave_flag = pm->wave_flag;
   a.chunks = pm->chunks;
   a.ctl = pm->chunks + cgpu::nat64_ctl_offset(pm->scratch_n) / 4u;
   a.stash_key = pm->stash_key;

@@ -89,6 +89,10 @@ struct Nat64Args {
   uint8_t *disposition;
   uint8_t *status;
   uint32_t *pkt_slot;    // scratch [n]: table slot (| kLocalBit: a key new in this batch), or 0xffffffff
+  uint8_t *wave_flag;    // scratch [n / 32 + 1]: 1 if the fused kernel's wave of 32 frames wrote
+                         // their pkt_slot entries (it had a deferred frame), else 0: the
+                         // entries are stale and read as 0xffffffff (the steady state
+                         // writes no pkt_slot at all)
   uint32_t *chunks;      // scratch [10 nblocks + n (rounded up to 32) + 33 * 32]: the tail's
                          // chunk counts, bases, first-packet masks, its list of tag
                          // collisions, then its control lines (zero between calls)
