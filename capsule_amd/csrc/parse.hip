@@ -140,6 +140,21 @@ __device__ __forceinline__ uint32_t chunk_excess(u32x4 v, uint32_t c, uint32_t f
   return e;
 }
 
+// Masks a 16-B chunk at its frame's end: bytes [rem, 16) become 0 (rem >= 16:
+// none).  Dword t keeps its low 8 * clamp(rem - 4 t, 0, 4) bits: the low half
+// of 2^32 - 1 shifted right by the dropped bits as a 64-bit value (a shift by
+// 32 gives 0, where a 32-bit shift would wrap), 4 VALU per dword against 7
+// for two compares and two selects.
+__device__ __forceinline__ void mask_chunk(u32x4 &v, uint32_t rem) {
+  const int r8 = 8 * (int)(rem < 16u ? rem : 16u);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    int sh = 32 * t + 32 - r8;
+    sh = sh < 0 ? 0 : (sh > 32 ? 32 : sh);
+    v[t] &= (uint32_t)(0xffffffffull >> sh);
+  }
+}
+
 // ---- the rows path (L4 checksum configs, waves of long frames) -----------
 // A wave whose frames are 16-B aligned and at least half of them 128 B or
 // longer reads each frame's first 512 B once, in rows: 16 lanes
@@ -191,13 +206,7 @@ __device__ __forceinline__ void rows_prologue(rsrc_t rs, uint32_t off, uint32_t 
           const uint32_t b0 = 256u * p + 16u * l;
           const uint32_t rem = fl[u] > b0 ? fl[u] - b0 : 0u;
           u32x4 x4 = v[u];
-          if (__ballot(rem < 16u)) {
-#pragma unroll
-            for (uint32_t t = 0; t < 4u; ++t) {
-              const uint32_t lo = 4u * t;
-              x4[t] &= rem >= lo + 4u ? 0xffffffffu : (rem <= lo ? 0u : 0xffffffffu >> (8u * (lo + 4u - rem)));
-            }
-          }
+          if (__ballot(rem < 16u)) mask_chunk(x4, rem);
           uint32_t x = sum4(x4, 0u);
           x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, true);  // row_shr:1
           x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, true);  // row_shr:2
@@ -340,17 +349,11 @@ __device__ __forceinline__ void stream_prologue(rsrc_t rs, uint32_t base, uint32
       for (uint32_t u = 0; u < kStreamU; ++u) {
         const uint32_t rel = 16u * k[u].c;
         const uint32_t rem = k[u].c < hi && rel < k[u].fe ? k[u].fe - rel : 16u;
-        if (__ballot(rem < 16u)) {
-#pragma unroll
-          for (uint32_t t = 0; t < 4u; ++t) {
-            const uint32_t b = 4u * t;
-            v[u][t] &= rem >= b + 4u ? 0xffffffffu : (rem <= b ? 0u : 0xffffffffu >> (8u * (b + 4u - rem)));
-          }
-        }
+        if (__ballot(rem < 16u)) mask_chunk(v[u], rem);
         // bytes 0..95 of a frame of this half: its window
         const uint32_t pos = rel - fst[k[u].own], fh = k[u].own - kRowHalf * half;
         if (k[u].c < hi && pos < 96u && fh < kRowHalf)
-          *reinterpret_cast<u32x4 *>(win + fh * kWin + (pos >> 2)) = v[u];
+          *reinterpret_cast<u32x4 *>(win + __umul24(fh, kWin) + (pos >> 2)) = v[u];
         const uint32_t p = wave_scan_incl(sum4(v[u], 0u));
         const uint32_t own = k[u].own;
         const uint32_t own_prev = dpp_wave_shr1(own), own_next = dpp_wave_shl1(own);
@@ -1038,8 +1041,12 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
     const bool rec = valid && (uint64_t)off + len <= (uint64_t)a.arena_len &&
                      (L4C ? l4_ok
                                    : (a.depth >= CGPU_LAYER_L3 ? l3_ok : eth_ok && ((mi >> 8) & 0xffu) != 0u));
-    // the fields reconcile writes: frame position and big-endian value
-    uint32_t fp[4], fv[4], nf = 0;
+    // the fields reconcile writes: frame position and big-endian value, in
+    // fixed slots (L4 first / second, L3 first / second; kNoField: none) so
+    // that every index is a compile-time constant and the arrays stay in
+    // registers
+    constexpr uint32_t kNoField = 0xffffu;
+    uint32_t fp[4] = {kNoField, kNoField, kNoField, kNoField}, fv[4] = {0u, 0u, 0u, 0u};
     if (rec) {
       if (L4C) {
         if (udp) {
@@ -1047,22 +1054,20 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
           fv[0] = span16;
           fp[1] = l4_off + 6u;
           fv[1] = l4_c;
-          nf = 2;
         } else {
           fp[0] = l4_off + (tcp ? 16u : 2u);
           fv[0] = l4_c;
-          nf = 1;
         }
       }
       if (a.depth >= CGPU_LAYER_L3) {
         if (v6) {
-          fp[nf] = eth_len + 4u;
-          fv[nf++] = (len - eth_len - 40u) & 0xffffu;
+          fp[2] = eth_len + 4u;
+          fv[2] = (len - eth_len - 40u) & 0xffffu;
         } else {
-          fp[nf] = eth_len + 2u;
-          fv[nf++] = (len - eth_len) & 0xffffu;
-          fp[nf] = eth_len + 10u;
-          fv[nf++] = ip_c;
+          fp[2] = eth_len + 2u;
+          fv[2] = (len - eth_len) & 0xffffu;
+          fp[3] = eth_len + 10u;
+          fv[3] = ip_c;
         }
       }
     }
@@ -1087,7 +1092,7 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
       const uint64_t wm = __ballot(whole);
       uint32_t pf[4];  // field: position << 16 | big-endian value (none: 0xffff0000)
 #pragma unroll
-      for (uint32_t q = 0; q < 4u; ++q) pf[q] = whole && q < nf && fp[q] < 64u ? (fp[q] << 16) | fv[q] : 0xffff0000u;
+      for (uint32_t q = 0; q < 4u; ++q) pf[q] = whole && fp[q] < 64u ? (fp[q] << 16) | fv[q] : 0xffff0000u;
       const rsrc_t ws = make_rsrc(a.wr_arena, a.arena_len);
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #pragma unroll
@@ -1117,7 +1122,7 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
       // behind tags, its TCP checksum)
 #pragma unroll
       for (uint32_t q = 0; q < 4u; ++q)
-        if (q < nf && (!stored || fp[q] >= 64u)) st16be(f + fp[q], fv[q]);
+        if (fp[q] != kNoField && (!stored || fp[q] >= 64u)) st16be(f + fp[q], fv[q]);
     }
     if (valid && a.rstatus != nullptr) a.rstatus[i] = rec ? CGPU_RECON_OK : CGPU_RECON_SKIPPED;
     return;
