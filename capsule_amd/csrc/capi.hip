@@ -98,7 +98,80 @@ struct cgpu_ctx {
   cgpu::HostRegion reg[cgpu::kMaxRegions];
   bool reg_owned[cgpu::kMaxRegions];  // registered here (else: already page-locked)
   uint32_t nreg = 0;
+  // The rows kernels' wave schedules (kernels.hpp ParseArgs::sched): waves
+  // resident on this device, and one granule buffer per stream the context
+  // has launched on, with the tag of its latest call.  Calls on one stream
+  // run in order, so no buffer is ever read by two calls at once.  Streams
+  // are told apart by id where the HIP runtime can tell (hipStreamGetId, ids
+  // are never reused), else by handle.
+  uint32_t resident_waves = 0;
+  struct Sched {
+    unsigned long long key;
+    unsigned long long *buf;
+    uint32_t tag;
+  };
+  std::vector<Sched> sched;
 };
+
+namespace {
+
+// Resident waves of the rows kernels: the CU count x 32 (8 waves per SIMD),
+// or CGPU_TEST_SCHED_WAVES (test hook: a decimal 64..2^20, so that small
+// batches run several rounds of waves and take the schedule).
+uint32_t resident_waves(int device) {
+  if (const char *e = getenv("CGPU_TEST_SCHED_WAVES")) {
+    char *end = nullptr;
+    const unsigned long v = strtoul(e, &end, 10);
+    if (end != e && *end == '\0' && v >= 64ul && v <= (1ul << 20)) {
+      fprintf(stderr, "capsule_gpu: test hook CGPU_TEST_SCHED_WAVES=%lu active\n", v);
+      return (uint32_t)v;
+    }
+    fprintf(stderr, "capsule_gpu: ignoring malformed CGPU_TEST_SCHED_WAVES\n");
+  }
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+    return 0;
+  return (uint32_t)cus * cgpu::kResidentWavesPerCU;
+}
+
+// Gives a call of a.n frames on `stream` its wave schedule when the launch
+// is more than one round of waves: the last min(groups - resident,
+// kSchedMax) groups of 64 frames, rounded down to whole lists of 256, are
+// ordered longest span first (parse.hip).  The kernel ignores it unless it
+// runs the rows variant.
+int set_schedule(cgpu_ctx *c, cgpu::ParseArgs &a, void *stream) {
+  a.sched = nullptr;
+  const uint32_t groups = (a.n + 63u) / 64u;
+  if (c->resident_waves == 0 || groups <= c->resident_waves) return 0;
+  // whole lists of 256 groups (one ordering workgroup each)
+  const uint32_t over = groups - c->resident_waves;
+  const uint32_t n_sched = (over < cgpu::kSchedMax ? over : cgpu::kSchedMax) / 256u * 256u;
+  if (n_sched == 0) return 0;
+  const unsigned long long sid = stream_id(stream);
+  const unsigned long long key = sid ? sid : (unsigned long long)(uintptr_t)stream | (1ull << 63);
+  cgpu_ctx::Sched *b = nullptr;
+  for (auto &x : c->sched)
+    if (x.key == key) b = &x;
+  if (!b) {
+    unsigned long long *buf = nullptr;
+    const size_t bytes = sizeof(unsigned long long) * cgpu::kSchedMax;
+    if (hipMalloc((void **)&buf, bytes) != hipSuccess) return CGPU_ENOMEM;
+    if (hipMemset(buf, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(buf);
+      return CGPU_EIO;
+    }
+    c->sched.push_back(cgpu_ctx::Sched{key, buf, 0u});
+    b = &c->sched.back();
+  }
+  if (++b->tag == 0u) b->tag = 1u;  // tags are never 0: a zeroed granule matches no call
+  a.sched = b->buf;
+  a.sched_n = n_sched;
+  a.sched_from = groups - n_sched;
+  a.sched_tag = b->tag;
+  return 0;
+}
+
+}  // namespace
 
 struct cgpu_portmap {
   cgpu_ctx *ctx;
@@ -179,6 +252,7 @@ int cgpu_ctx_create(int hip_device, cgpu_ctx **out) {
   cgpu_ctx *c = new (std::nothrow) cgpu_ctx();
   if (!c) return fail(CGPU_ENOMEM);
   c->device = hip_device;
+  c->resident_waves = resident_waves(hip_device);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(CGPU_EIO);
@@ -195,6 +269,7 @@ void cgpu_ctx_destroy(cgpu_ctx *c) {
   if (c->h_desc) (void)hipHostFree(c->h_desc);
   if (c->d_desc) (void)hipFree(c->d_desc);
   if (c->gb_counts) (void)hipFree(c->gb_counts);
+  for (auto &x : c->sched) (void)hipFree(x.buf);
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_zc) (void)hipFree(c->d_zc);
   for (uint32_t r = 0; r < c->nreg; ++r)
@@ -237,6 +312,7 @@ int cgpu_parse_batch(cgpu_ctx *ctx, const cgpu_batch *batch, uint32_t flags,
   a.hash = out->flow_hash;
   a.fields = out->fields;
   a.ext = out->ext;
+  if (int e = set_schedule(ctx, a, stream)) return fail(e);
   hipError_t e = cgpu::launch_parse(a, flags, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e);
   return ok();
@@ -1099,6 +1175,7 @@ int cgpu_reconcile(cgpu_ctx *ctx, uint8_t *arena, uint64_t arena_len, const uint
   a.meta_in = meta;
   a.depth = depth;
   a.rstatus = status;
+  if (int e = set_schedule(ctx, a, stream)) return fail(e);
   hipError_t e = cgpu::launch_reconcile(a, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e);
   return ok();
@@ -1185,6 +1262,7 @@ int cgpu_reconcile_frames(cgpu_ctx *ctx, uint8_t *const *frames, const uint16_t 
     a.meta_in = (const uint32_t *)(D + o_meta);
     a.depth = depth;
     a.rstatus = D + o_st;
+    if (int e = set_schedule(ctx, a, s)) return fail(e);
     hipError_t e = cgpu::launch_reconcile(a, s);
     if (e != hipSuccess) return hip_fail(e);
     if (hipMemcpyAsync(H + o_st, D + o_st, m, hipMemcpyDeviceToHost, s) != hipSuccess ||

@@ -30,7 +30,20 @@ struct ParseArgs {
   const uint32_t *meta_in = nullptr;
   uint32_t depth = 0;
   uint8_t *rstatus = nullptr;
+  // The rows kernels' wave order (parse.hip, "Longest span first"): a wave
+  // takes a group of 64 frames; waves sched_from .. sched_from + sched_n - 1
+  // take the groups the launch's first sched_n / 256 workgroups order for
+  // them, longest span first, through 8-byte granules {tag, group} in
+  // `sched`.  nullptr: every wave takes the group of its own index.
+  unsigned long long *sched = nullptr;
+  uint32_t sched_from = 0, sched_n = 0;
+  uint32_t sched_tag = 0;  // this call's granule tag (never 0)
 };
+
+// Waves the rows kernels keep resident per CU (8 waves per SIMD), and the
+// most waves one launch orders (the granules of one schedule buffer).
+constexpr uint32_t kResidentWavesPerCU = 32;
+constexpr uint32_t kSchedMax = 8192;
 
 hipError_t launch_parse(const ParseArgs &a, uint32_t flags, hipStream_t s);
 // Packet::reconcile_all at a.depth (accept set in a.accept).

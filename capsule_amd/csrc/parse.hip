@@ -379,6 +379,115 @@ __device__ __forceinline__ void stream_prologue(rsrc_t rs, uint32_t base, uint32
   s_all = acc[lane];
 }
 
+// ---- Longest span first: the order of the last round of waves ------------
+// A wave takes 64 consecutive frames, and on the stream / rows paths its time
+// follows its span (the bytes from its first frame's start to its last
+// frame's end): for shuffled IMIX 11 to 37 KB.  A 1 Mi-packet launch is
+// 16,384 waves, two per wave slot of the chip, and the waves dispatched last
+// decide when it ends: with the groups taken in their own order the launch
+// took 86.7 us, with the last half of them taken longest span first 77.3 us
+// (tools/imix_order_probe.py).  So the launch's first
+// sched_n / 256 workgroups each order 256 of the last sched_n groups by span,
+// longest first (64 classes a quarter octave wide; a counting sort in LDS,
+// one atomic per class present in a wave, never one per lane), and the k-th
+// group of list b goes to the wave at position k * lists + b of the ordered
+// range: the lists interleave into about the global order with no exchange
+// between workgroups.  A wave learns its group from granule q: 8 bytes
+// {tag, group} written by ONE write-through (sc1) store and polled by ONE
+// lane with sc1 loads, so no fence orders anything (the R2 granule of
+// cdna_hip_programming.md Guideline 16).  The tag is the call's own (the host
+// counts calls per buffer), so a granule an earlier call left never matches.
+// Which wave takes which group changes no output: every frame's results are
+// its own.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+constexpr uint32_t kSchedClasses = 64;
+constexpr uint32_t kSpinMax = 1u << 24;  // granule polls before a wave gives up (seconds)
+
+__device__ __forceinline__ uint32_t span_class(uint32_t span) {
+  // quarter octaves, longest first: class 0 holds spans of 16 MiB and more,
+  // class 63 those below 304 B
+  const uint32_t s = span < 16u ? 16u : span;
+  const uint32_t msb = 31u - (uint32_t)__builtin_clz(s);
+  const uint32_t q = 4u * msb + ((s >> (msb - 2u)) & 3u);  // 16 .. 127
+  return q >= 96u ? 0u : (q <= 33u ? kSchedClasses - 1u : 96u - q);
+}
+
+// Adds each lane's count to ctr[its class] with one LDS atomic per class the
+// wave holds; returns the counter's value before this wave's add plus the
+// lane's rank among the wave's lanes of its class (lanes with in == false
+// take no part).
+__device__ __forceinline__ uint32_t class_add(uint32_t *ctr, uint32_t c, bool in) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t left = __ballot(in);
+  uint32_t pos = 0;
+  while (left) {
+    const uint32_t first = (uint32_t)__builtin_ctzll(left);
+    const uint32_t cc = __builtin_amdgcn_readlane(c, (int)first);
+    const uint64_t m = __ballot(in && c == cc);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(&ctr[cc], (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, (int)first);
+    if (in && c == cc) pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    left &= ~m;
+  }
+  return pos;
+}
+
+__device__ void schedule_waves(const ParseArgs &a, uint32_t *L) {
+  uint32_t *cnt = L, *cur = L + kSchedClasses;
+  const uint32_t t = threadIdx.x, lists = a.sched_n / kBlock, j = kBlock * blockIdx.x + t;
+  if (t < kSchedClasses) cnt[t] = 0u;
+  const uint64_t nb = (uint64_t)a.n;
+  const rsrc_t r_off = make_rsrc(a.off, (uint32_t)(4u * nb < 0xffffffffull ? 4u * nb : 0xffffffffull));
+  const rsrc_t r_len = make_rsrc(a.len, (uint32_t)(2u * nb < 0xffffffffull ? 2u * nb : 0xffffffffull));
+  const uint32_t g = a.sched_from + j;
+  const uint32_t f0 = 64u * g, f1 = (f0 + 63u < a.n ? f0 + 63u : a.n - 1u);
+  const uint32_t o0 = __builtin_amdgcn_raw_buffer_load_b32(r_off, (int)(4u * f0), 0, 0);
+  const uint32_t o1 = __builtin_amdgcn_raw_buffer_load_b32(r_off, (int)(4u * f1), 0, 0);
+  const uint32_t l1 = __builtin_amdgcn_raw_buffer_load_b16(r_len, (int)(2u * f1), 0, 0);
+  // frames out of order (no stream path): the lightest class
+  const uint32_t c = o1 >= o0 ? span_class(o1 + l1 - o0) : kSchedClasses - 1u;
+  __syncthreads();
+  (void)class_add(cnt, c, true);
+  __syncthreads();
+  if (t < 64u) {  // exclusive prefix over the classes (one wave, 64 classes)
+    const uint32_t x = cnt[t];
+    uint32_t y = x;
+#pragma unroll
+    for (uint32_t d = 1; d < 64u; d <<= 1) {
+      const uint32_t z = (uint32_t)__shfl_up((int)y, d);
+      if (t >= d) y += z;
+    }
+    cur[t] = y - x;
+  }
+  __syncthreads();
+  const uint32_t k = class_add(cur, c, true);  // the group's rank in this list, longest first
+  __hip_atomic_store((gu64 *)(a.sched + k * lists + blockIdx.x), ((unsigned long long)a.sched_tag << 32) | g,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The group of 64 frames this wave takes (wave-uniform); ~0u: none (a wave
+// that gave up waiting for its granule).
+__device__ __forceinline__ uint32_t wave_group(const ParseArgs &a) {
+  if (a.sched == nullptr) return blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6);
+  const uint32_t v = (blockIdx.x - a.sched_n / kBlock) * (kBlock / 64u) + (threadIdx.x >> 6);
+  const uint32_t q = v - a.sched_from;
+  if (v < a.sched_from || q >= a.sched_n) return v;
+  uint32_t g = ~0u;
+  if ((threadIdx.x & 63u) == 0u) {
+    for (uint32_t spins = 0; spins < kSpinMax; ++spins) {
+      const unsigned long long x = __hip_atomic_load((gu64 *)(a.sched + q), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)(x >> 32) == a.sched_tag) {
+        g = (uint32_t)x;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  return (uint32_t)__shfl((int)g, 0);
+}
+
 // V4U: the accept set has no IPv6, TCP, ICMP or extension bit (the typed
 // parse::<Ipv4>() -> parse::<Udp<Ipv4>>() chain of the reference bench,
 // bench/packets.rs:65-69): every IPv6 / TCP / ICMP branch is compiled out,
@@ -400,7 +509,17 @@ __device__ __forceinline__ void st16be(uint8_t *p, uint32_t v) {
 // IPv4 total_length), and the lane stores the new fields into its frame.
 template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT, bool V4U, bool ROWS, bool RECON>
 __device__ __forceinline__ void parse_body(const ParseArgs &a) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  constexpr uint32_t kPathLds = kRowLds > kStreamLds ? kRowLds : kStreamLds;
+  __shared__ uint32_t rlds[ROWS ? kBlock / 64 : 1][ROWS ? kPathLds : 1];
+  if constexpr (ROWS) {
+    static_assert((kBlock / 64) * kPathLds >= 2u * kSchedClasses, "the schedule's LDS");
+    if (a.sched != nullptr && blockIdx.x < a.sched_n / kBlock) {
+      schedule_waves(a, &rlds[0][0]);
+      return;
+    }
+  }
+  const uint32_t grp = ROWS ? wave_group(a) : blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6);
+  const uint32_t i = grp == ~0u ? ~0u : 64u * grp + (threadIdx.x & 63u);
   // No early exit: lanes past n run with len 0 (status BadOffset) and store
   // nothing, so the wave stays whole for the cooperative tail sum below.
   const bool valid = i < a.n;
@@ -438,8 +557,6 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
     stream = !rows && stream_wave(off, len, valid, threadIdx.x & 63u, a.arena_len, st_base, st_span);
   }
   const bool slow = (off & 3u) != 0u || (uint64_t)off + 96u > (uint64_t)a.arena_len;
-  constexpr uint32_t kPathLds = kRowLds > kStreamLds ? kRowLds : kStreamLds;
-  __shared__ uint32_t rlds[ROWS ? kBlock / 64 : 1][ROWS ? kPathLds : 1];
   if (ROWS && rows) {
     rows_prologue(rs, valid ? off : 0u, valid ? len : 0u, threadIdx.x & 63u, rlds[threadIdx.x >> 6], P, s_all);
   } else if (ROWS && stream) {
@@ -1355,17 +1472,31 @@ __global__ __launch_bounds__(kBlock, 8) void recon_rows_kernel(ParseArgs a) {
   parse_body<true, L4C, false, false, EXT, V4U, true, true>(a);
 }
 
+// The rows path is compiled into a variant that the checksum configs get when
+// the batch's mean slot (arena bytes per packet) is 128..2200 B: long frames,
+// but not jumbo ones; each wave still decides by its own frames.
+bool rows_variant(const ParseArgs &a) {
+  const uint64_t mean = (uint64_t)a.arena_len / a.n;
+  return mean >= 128u && mean <= kRowsMeanMax;
+}
+
+// The launch of a rows kernel: sched_n / 256 workgroups more (they order the
+// waves) when the host gave it a schedule buffer.
+uint32_t rows_grid(const ParseArgs &a) {
+  return (a.n + kBlock - 1) / kBlock + (a.sched != nullptr ? a.sched_n / kBlock : 0u);
+}
+
 template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT, bool V4U>
 hipError_t launch_t(const ParseArgs &a, hipStream_t s) {
-  const uint32_t grid = (a.n + kBlock - 1) / kBlock;
-  // The rows path is compiled into a variant that the checksum configs get
-  // when the batch's mean slot (arena bytes per packet) is 128..2200 B: long
-  // frames, but not jumbo ones; each wave still decides by its own frames.
-  const uint64_t mean = (uint64_t)a.arena_len / a.n;
-  if (L4C && mean >= 128u && mean <= kRowsMeanMax)
-    hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, V4U, true>), dim3(grid), dim3(kBlock), 0, s, a);
-  else
-    hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, V4U, false>), dim3(grid), dim3(kBlock), 0, s, a);
+  if (L4C && rows_variant(a)) {
+    hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, V4U, true>), dim3(rows_grid(a)), dim3(kBlock), 0,
+                       s, a);
+  } else {
+    ParseArgs b = a;
+    b.sched = nullptr;
+    hipLaunchKernelGGL((parse_kernel<IPC, L4C, HASH, FIELDS, EXT, V4U, false>), dim3((a.n + kBlock - 1) / kBlock),
+                       dim3(kBlock), 0, s, b);
+  }
   return hipGetLastError();
 }
 
@@ -1390,12 +1521,13 @@ hipError_t launch_h(const ParseArgs &a, bool hash, bool fields, bool ext, hipStr
 
 template <bool L4C, bool EXT, bool V4U>
 hipError_t launch_recon_t(const ParseArgs &a, hipStream_t s) {
-  const uint32_t grid = (a.n + kBlock - 1) / kBlock;
-  const uint64_t mean = (uint64_t)a.arena_len / a.n;
-  if (L4C && mean >= 128u && mean <= kRowsMeanMax)
-    hipLaunchKernelGGL((recon_rows_kernel<L4C, EXT, V4U>), dim3(grid), dim3(kBlock), 0, s, a);
-  else
-    hipLaunchKernelGGL((recon_kernel<L4C, EXT, V4U>), dim3(grid), dim3(kBlock), 0, s, a);
+  if (L4C && rows_variant(a)) {
+    hipLaunchKernelGGL((recon_rows_kernel<L4C, EXT, V4U>), dim3(rows_grid(a)), dim3(kBlock), 0, s, a);
+  } else {
+    ParseArgs b = a;
+    b.sched = nullptr;
+    hipLaunchKernelGGL((recon_kernel<L4C, EXT, V4U>), dim3((a.n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b);
+  }
   return hipGetLastError();
 }
 

@@ -1,0 +1,132 @@
+"""The rows kernels' longest-span-first wave order (parse.hip, "Longest span
+first"): a launch of more than one round of waves has its last groups of 64
+frames ordered by its first workgroups and handed to the waves through
+granules.  The order must change no output.
+
+The bench-size batches (1 Mi frames, 16,384 groups against 8,192 resident
+waves) take the schedule in tests/test_bench_parity_gpu.py and
+tests/test_reconcile_gpu.py.  Here the test hook CGPU_TEST_SCHED_WAVES
+(read when a context is created) makes small batches take it: with 256
+resident waves, a batch of 600 groups has its last 256 ordered (whole
+lists of 256 groups, one ordering workgroup each).  Covered:
+IMIX (stream path), 256-B and 1500-B frames (rows path), out-of-order
+descriptors (window path; the scheduler's lightest class), a partial last
+group, reconcile on stale IMIX, more groups than one schedule holds, and two
+streams of one context at once (one granule buffer per stream).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib
+from capsule_amd import _native as N
+from capsule_amd import packets, synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+FLAGS = N.F_ACCEPT_ALL | N.F_FLOW_HASH | N.F_CSUM_IP | N.F_CSUM_L4
+
+
+@pytest.fixture(scope="module")
+def sctx():
+    os.environ["CGPU_TEST_SCHED_WAVES"] = "256"
+    try:
+        c = packets.Context(0)
+    finally:
+        del os.environ["CGPU_TEST_SCHED_WAVES"]
+    yield c
+    c.close()
+
+
+def _check_parse(c, arena, off, ln, flags=FLAGS, stream=None):
+    b = packets.PacketBatch.from_numpy(arena, off, ln, DEV)
+    r = packets.parse(c, b, flags=flags, stream=stream)
+    torch.cuda.synchronize()
+    om, oc, oh, _ = oracle_lib.parse_batch(arena, off, ln, flags, fields=False)
+    for name, got, want in (("meta", r.meta.cpu().numpy().view(np.uint32), om),
+                            ("csum", r.csum.cpu().numpy().view(np.uint32), oc),
+                            ("flow hash", r.flow_hash.cpu().numpy().view(np.uint64), oh)):
+        bad = np.nonzero(got != want)[0]
+        assert not len(bad), f"{name} differs at {bad[:8]} of {len(got)}"
+    return om
+
+
+def _shuffle_groups(arena, off, ln, seed):
+    """The same frames with their descriptors' 64-frame groups permuted: the
+    groups keep their spans, the batch's order of them changes."""
+    g = len(off) // 64
+    perm = np.random.default_rng(seed).permutation(g)
+    idx = np.concatenate([(perm[:, None] * 64 + np.arange(64)[None, :]).reshape(-1),
+                          np.arange(64 * g, len(off))])
+    return arena, off[idx].copy(), ln[idx].copy()
+
+
+@pytest.mark.parametrize("n", [64 * 600, 64 * 600 + 17, 64 * 257 + 1])
+def test_imix_stream_path(sctx, n):
+    arena, off, ln = synth.imix(n, seed=n)
+    om = _check_parse(sctx, arena, off, ln)
+    assert (om & 0xFF == 0).all()
+
+
+@pytest.mark.parametrize("size", [256, 1500])
+def test_uniform_rows_path(sctx, size):
+    arena, off, ln = synth.uniform(64 * 600, frame_len=size, slot=(size + 63) // 64 * 64, seed=size)
+    _check_parse(sctx, arena, off, ln, flags=N.F_ACCEPT_V4 | N.F_ACCEPT_UDP | N.F_CSUM_IP
+                 | N.F_CSUM_L4 | N.F_FLOW_HASH)
+
+
+def test_groups_out_of_order(sctx):
+    """Groups permuted, and one group's frames reversed (no stream path; the
+    scheduler puts it in its lightest class)."""
+    arena, off, ln = synth.imix(64 * 600, seed=11)
+    arena, off, ln = _shuffle_groups(arena, off, ln, 3)
+    off[64 * 500:64 * 501] = off[64 * 500:64 * 501][::-1].copy()
+    ln[64 * 500:64 * 501] = ln[64 * 500:64 * 501][::-1].copy()
+    _check_parse(sctx, arena, off, ln)
+
+
+def test_more_groups_than_one_schedule(sctx):
+    """256 resident waves, 8,192 ordered at most: a batch of 9,000 groups
+    runs groups 256 .. 807 in their own order and orders the last 8,192."""
+    arena, off, ln = synth.imix(64 * 9000, seed=5)
+    _check_parse(sctx, arena, off, ln)
+
+
+def test_reconcile_stale_imix(sctx):
+    arena, off, ln = synth.imix(64 * 600 + 5, seed=9)
+    b = packets.PacketBatch.from_numpy(arena, off, ln, DEV)
+    flags = N.F_ACCEPT_ALL | N.F_ACCEPT_ICMP
+    r = packets.parse(sctx, b, flags=flags)
+    meta = r.meta.cpu().numpy().view(np.uint32)
+    stale = arena.copy()
+    synth.stale_fields(stale, off, ln, meta, seed=4)
+    b = packets.PacketBatch.from_numpy(stale, off, ln, DEV)
+    st = packets.reconcile(sctx, b, r.meta, flags=flags, depth="l4")
+    want, want_st = oracle_lib.reconcile(stale, off, ln, meta, flags, N.LAYER_L4)
+    got = b.arena.cpu().numpy()
+    bad = np.nonzero(got != want)[0]
+    assert not len(bad), f"{len(bad)} bytes differ, first at {bad[:4]}"
+    assert (st.cpu().numpy() == want_st).all()
+
+
+def test_two_streams_at_once(sctx):
+    """Two streams of one context, launches interleaved without syncs: each
+    stream has its own granule buffer and tag sequence."""
+    batches = []
+    for seed in (21, 22):
+        arena, off, ln = synth.imix(64 * 700, seed=seed)
+        batches.append((arena, off, ln, packets.PacketBatch.from_numpy(arena, off, ln, DEV)))
+    streams = [torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)]
+    outs = []
+    for k in range(6):
+        s = streams[k & 1]
+        arena, off, ln, b = batches[k & 1]
+        outs.append((k & 1, packets.parse(sctx, b, flags=FLAGS, stream=s)))
+    torch.cuda.synchronize()
+    for j, r in outs:
+        arena, off, ln, _ = batches[j]
+        om, oc, oh, _ = oracle_lib.parse_batch(arena, off, ln, FLAGS, fields=False)
+        assert (r.meta.cpu().numpy().view(np.uint32) == om).all()
+        assert (r.flow_hash.cpu().numpy().view(np.uint64) == oh).all()
