@@ -237,7 +237,11 @@ void cgpu_ctx_destroy(cgpu_ctx *ctx);
  * (udp.rs:287 / tcp.rs:558), plus Ipv4::compute_checksum (v4.rs:322),
  * Udp/Tcp::compute_checksum (udp.rs:204 / tcp.rs:462) evaluated on the bytes
  * as they are, and the hash of Udp/Tcp::flow() (udp.rs:151, tcp.rs:409).
- * Asynchronous on `stream`.                                               */
+ * Asynchronous on `stream`.  A batch of more than one round of waves (64
+ * frames a wave, 32 waves resident per CU) with checksums over long frames
+ * orders its last waves longest span first through a 64 KB buffer the
+ * context keeps per stream; the first such call on a stream allocates it
+ * and synchronises the device once.  The results do not depend on it.    */
 int cgpu_parse_batch(cgpu_ctx *ctx, const cgpu_batch *batch, uint32_t flags,
                      const cgpu_parse_out *out, void *stream);
 
