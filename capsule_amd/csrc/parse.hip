@@ -1250,8 +1250,12 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
 
 }
 
+// The header-record (FIELDS) and extension (EXT) variants of the rows kernel,
+// and the window kernel with both, hold more state than 64 VGPRs at 8 waves
+// per SIMD and spilled 12-52 B per lane to scratch; they run at 6 (no spill).
 template <bool IPC, bool L4C, bool HASH, bool FIELDS, bool EXT, bool V4U, bool ROWS, bool RECON = false>
-__global__ __launch_bounds__(kBlock, 8) void parse_kernel(ParseArgs a) {
+__global__ __launch_bounds__(kBlock, ((ROWS && (FIELDS || EXT)) || (FIELDS && EXT)) ? 6 : 8) void parse_kernel(
+    ParseArgs a) {
   parse_body<IPC, L4C, HASH, FIELDS, EXT, V4U, ROWS, RECON>(a);
 }
 
