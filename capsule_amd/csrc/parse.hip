@@ -1463,7 +1463,11 @@ __device__ __forceinline__ bool recon_short(const ParseArgs &a) {
 // A/B against 8 (45.95 against 50.5 us at 1 Mi x 64 B) was within that
 // launch's run-to-run spread (44.9-50.0 us for 6 on one box), and with the
 // short path 6 and 8 time the same (32.6 us, round 5).  The rows variant
-// (IMIX) keeps 8: 126.2 us against 128.5 us at 6 (round 4, one box).
+// (IMIX) ran at 8 (126.2 us against 128.5 us at 6, round 4, one box) but
+// spilled 12-24 B per lane to scratch there; it runs at 7, where it does not
+// (no kernel of the library uses scratch memory: a launch whose scratch
+// need differs from the one before it makes the runtime re-size the queue's
+// scratch).
 template <bool L4C, bool EXT, bool V4U>
 __global__ __launch_bounds__(kBlock, 6) void recon_kernel(ParseArgs a) {
   if constexpr (L4C) {
@@ -1472,7 +1476,7 @@ __global__ __launch_bounds__(kBlock, 6) void recon_kernel(ParseArgs a) {
   parse_body<true, L4C, false, false, EXT, V4U, false, true>(a);
 }
 template <bool L4C, bool EXT, bool V4U>
-__global__ __launch_bounds__(kBlock, 8) void recon_rows_kernel(ParseArgs a) {
+__global__ __launch_bounds__(kBlock, 7) void recon_rows_kernel(ParseArgs a) {
   parse_body<true, L4C, false, false, EXT, V4U, true, true>(a);
 }
 
