@@ -385,6 +385,20 @@ def nat64_replies(out_arena, off, out_len):
     return a, off.astype(np.uint32), out_len.astype(np.uint16)
 
 
+def host_buffer(nbytes):
+    """A zeroed u8 array of its own pages (an anonymous mmap, page-aligned,
+    sharing no page with any other allocation), for host memory that gets
+    registered with the GPU (hipHostRegister pins whole pages: a malloc'd
+    array would pin, and after unregistering leave, pages that the Python
+    heap shares with later allocations -- torch copies' host buffers among
+    them).  The mapping lives as long as the array."""
+    import mmap
+
+    size = max(int(nbytes), 1)
+    m = mmap.mmap(-1, (size + mmap.PAGESIZE - 1) // mmap.PAGESIZE * mmap.PAGESIZE)
+    return np.frombuffer(m, dtype=np.uint8, count=size)
+
+
 def mbuf_pool(arena, off, length, mem=None, headroom=128, seed=7, room=None):
     """Lay a batch out as a DPDK-style mempool in host memory: one object per
     packet = a 128-B rte_mbuf header (buf_addr @0, data_off @16, pkt_len @36,
@@ -393,7 +407,7 @@ def mbuf_pool(arena, off, length, mem=None, headroom=128, seed=7, room=None):
     default is 2048), object stride a multiple of 64, objects in shuffled
     order (a pool hands out buffers in no particular order).  `mem`: a u8
     array to build in (e.g. a pinned torch tensor's numpy view), else a new
-    numpy array.  Returns (mem, mbufs u64[n] = the rte_mbuf addresses in
+    array of its own pages (host_buffer).  Returns (mem, mbufs u64[n] = the rte_mbuf addresses in
     batch order)."""
     n = len(off)
     length = np.asarray(length, dtype=np.int64)
@@ -402,7 +416,7 @@ def mbuf_pool(arena, off, length, mem=None, headroom=128, seed=7, room=None):
     stride = (128 + headroom + room + 63) // 64 * 64
     need = max(stride * n, 64)
     if mem is None:
-        mem = np.zeros(need, np.uint8)
+        mem = host_buffer(need)
     assert mem.nbytes >= need and mem.dtype == np.uint8
     base = mem.ctypes.data
     objs = np.random.default_rng(seed).permutation(n).astype(np.int64) * stride

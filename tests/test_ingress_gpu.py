@@ -146,7 +146,7 @@ def test_register_unregister_bookkeeping(ctx):
     L = N.lib()
     buf = np.zeros(1 << 16, np.uint8)
     assert L.cgpu_host_unregister(ctx.handle, ctypes.c_void_p(buf.ctypes.data)) == N.EINVAL
-    bufs = [np.zeros(4096, np.uint8) for _ in range(17)]
+    bufs = [synth.host_buffer(4096) for _ in range(17)]
     regs = []
     try:
         for b in bufs[:16]:
