@@ -396,7 +396,9 @@ __device__ __forceinline__ void stream_prologue(rsrc_t rs, uint32_t base, uint32
 // {tag, group} written by ONE write-through (sc1) store and polled by ONE
 // lane with sc1 loads, so no fence orders anything (the R2 granule of
 // cdna_hip_programming.md Guideline 16).  The tag is the call's own (the host
-// counts calls per buffer), so a granule an earlier call left never matches.
+// counts calls per buffer), and the wave that takes a granule clears it, so
+// an entry an earlier launch left never matches, even one replayed from a
+// captured graph with the same tag.
 // Which wave takes which group changes no output: every frame's results are
 // its own.
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -480,6 +482,9 @@ __device__ __forceinline__ uint32_t wave_group(const ParseArgs &a) {
                                                      __HIP_MEMORY_SCOPE_AGENT);
       if ((uint32_t)(x >> 32) == a.sched_tag) {
         g = (uint32_t)x;
+        // consumed: cleared for the next launch, so that a launch replayed
+        // with the same tag (a captured graph) never reads this one's entry
+        __hip_atomic_store((gu64 *)(a.sched + q), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       __builtin_amdgcn_s_sleep(8);

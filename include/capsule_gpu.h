@@ -241,7 +241,9 @@ void cgpu_ctx_destroy(cgpu_ctx *ctx);
  * frames a wave, 32 waves resident per CU) with checksums over long frames
  * orders its last waves longest span first through a 64 KB buffer the
  * context keeps per stream; the first such call on a stream allocates it
- * and synchronises the device once.  The results do not depend on it.    */
+ * and synchronises the device once (so it must come before a graph capture
+ * on that stream; captured calls replay correctly).  The results do not
+ * depend on the order.                                                    */
 int cgpu_parse_batch(cgpu_ctx *ctx, const cgpu_batch *batch, uint32_t flags,
                      const cgpu_parse_out *out, void *stream);
 

@@ -11,8 +11,9 @@ resident waves, a batch of 600 groups has its last 256 ordered (whole
 lists of 256 groups, one ordering workgroup each).  Covered:
 IMIX (stream path), 256-B and 1500-B frames (rows path), out-of-order
 descriptors (window path; the scheduler's lightest class), a partial last
-group, reconcile on stale IMIX, more groups than one schedule holds, and two
-streams of one context at once (one granule buffer per stream).
+group, reconcile on stale IMIX, more groups than one schedule holds, two
+streams of one context at once (one granule buffer per stream), and graph
+replays (the captured tag; granules cleared by the waves that take them).
 """
 import os
 
@@ -130,3 +131,33 @@ def test_two_streams_at_once(sctx):
         om, oc, oh, _ = oracle_lib.parse_batch(arena, off, ln, FLAGS, fields=False)
         assert (r.meta.cpu().numpy().view(np.uint32) == om).all()
         assert (r.flow_hash.cpu().numpy().view(np.uint64) == oh).all()
+
+
+def test_graph_replay_with_new_frames(sctx):
+    """A parse captured into a graph replays with the tag it was captured
+    with; each wave clears the granule it took, so a replay never reads the
+    previous replay's entries.  Three replays over changed frame bytes, each
+    against the oracle."""
+    arena, off, ln = synth.imix(64 * 600, seed=31)
+    n = len(off)
+    b = packets.PacketBatch.from_numpy(arena, off, ln, DEV)
+    out = packets.ParseBuffers(n, DEV)
+    s = torch.cuda.Stream(DEV)
+    with torch.cuda.stream(s):
+        packets.parse(sctx, b, flags=FLAGS, out=out, stream=s)  # the stream's granule buffer
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        packets.parse(sctx, b, flags=FLAGS, out=out, stream=s)
+    rng = np.random.default_rng(5)
+    for _ in range(3):
+        ak = arena.copy()
+        hit = rng.integers(0, len(ak), 20_000)
+        ak[hit] ^= rng.integers(1, 256, len(hit), dtype=np.uint8)
+        b.arena.copy_(torch.from_numpy(ak))
+        g.replay()
+        torch.cuda.synchronize()
+        om, oc, oh, _ = oracle_lib.parse_batch(ak, off, ln, FLAGS, fields=False)
+        assert (out.meta.cpu().numpy().view(np.uint32) == om).all()
+        assert (out.csum.cpu().numpy().view(np.uint32) == oc).all()
+        assert (out.flow_hash.cpu().numpy().view(np.uint64) == oh).all()
