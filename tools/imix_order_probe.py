@@ -7,7 +7,11 @@ of its last), which for shuffled IMIX ranges from about 11 to 37 KB.  A
 waves dispatched last decide when the launch ends.  This probe times the
 same frames (same arena, same descriptors) with the 64-frame groups taken
 in three orders: as generated, longest span first (the order that leaves
-short waves for the end) and shortest first.  Diagnostic only:
+short waves for the end) and shortest first, and with only the groups after
+the first G taken longest first.  The committed logs
+(profiles/round5/imix_order_probe*.log) were taken before the kernel ordered
+its last round itself (parse.hip, "Longest span first"); with that order in
+place the probe measures the two orders stacked.  Diagnostic only:
 python tools/imix_order_probe.py [steps]
 """
 import os
@@ -38,6 +42,13 @@ def main():
     orders = {"generated": np.arange(len(span)),
               "longest_first": np.argsort(-span, kind="stable"),
               "shortest_first": np.argsort(span, kind="stable")}
+    # the first G groups as generated (the waves resident from the start),
+    # the rest longest first: what a schedule built during the first round
+    # could do for the second
+    for first in (4096, 6144, 8192, 10240):
+        rest = np.arange(first, len(span))
+        orders[f"gen{first}+longest"] = np.concatenate(
+            [np.arange(first), rest[np.argsort(-span[rest], kind="stable")]])
     for name, order in orders.items():
         idx = (order[:, None] * 64 + np.arange(64)[None, :]).reshape(-1)
         w = dict(w0, off=w0["off"][idx].copy(), len=w0["len"][idx].copy())
