@@ -795,10 +795,10 @@ def bench_nat64_mbufs(args, w):
     n = len(w["off"])
     room = 2048  # DPDK's default data room: 4to6 needs the tailroom
     stride = (128 + 128 + room + 63) // 64 * 64
-    pinned = torch.zeros(stride * n, dtype=torch.uint8, pin_memory=True)
-    mem, mbufs = synth.mbuf_pool(w["arena"], w["off"], w["len"], mem=pinned.numpy(), room=room)
+    pinned, pool = synth.pinned_buffer(stride * n)
+    mem, mbufs = synth.mbuf_pool(w["arena"], w["off"], w["len"], mem=pool, room=room)
     orig = mem.copy()
-    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    reg = packets.HostRegion.of(ctx, mem)
     if not to6:
         gw = packets.Nat64Gateway(ctx, capacity_log2=PORTMAP_LOG2)
     B = min(args.burst, n)
@@ -862,9 +862,9 @@ def e2e_mbufs(args):
     n = len(w["off"])
     ctx = packets.Context(0)
     stride = (128 + 128 + int(w["len"].max()) + 63) // 64 * 64
-    pinned = torch.zeros(stride * n, dtype=torch.uint8, pin_memory=True)
-    mem, mbufs = synth.mbuf_pool(w["arena"], w["off"], w["len"], mem=pinned.numpy())
-    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    pinned, pool = synth.pinned_buffer(stride * n)
+    mem, mbufs = synth.mbuf_pool(w["arena"], w["off"], w["len"], mem=pool)
+    reg = packets.HostRegion.of(ctx, mem)
     ingress = {"stage": N.INGRESS_STAGE, "zero_copy": N.INGRESS_ZERO_COPY,
                "frames": N.INGRESS_ZERO_COPY}[args.ingress]
     B = min(args.burst, n)

@@ -12,9 +12,13 @@ import pathlib
 
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ.get("CAPSULE_GPU_LIB", _HERE / "libcapsule_gpu.so"))
+# The test build (capi.hip with CGPU_TEST_HOOKS): environment hooks that the
+# GPU tests use to force rare paths.  Only tests load it (lib(test=True));
+# the product library reads no environment.
+TEST_LIB_PATH = _HERE / "libcapsule_gpu_test.so"
 
 # ---- constants (include/capsule_gpu.h) ------------------------------------
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 OK, EINVAL, ENOMEM, ENODEV, EIO, ENOSPC = 0, -22, -12, -19, -5, -28
 
@@ -132,21 +136,23 @@ EXPORTS = [
     "cgpu_pkt_status_str", "cgpu_abi_version", "cgpu_host_register", "cgpu_host_unregister",
     "cgpu_parse_mbufs", "cgpu_set_ip", "cgpu_nat64_mbufs", "cgpu_parse_frames",
     "cgpu_nat64_frames", "cgpu_portmap_reset", "cgpu_reconcile", "cgpu_reconcile_frames",
+    "cgpu_ctx_check",
 ]
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    """Load libcapsule_gpu.so once; raise if it is absent (no fallback)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not LIB_PATH.exists():
+def lib(test=False):
+    """Load libcapsule_gpu.so (test=True: the test build) once; raise if it
+    is absent (no fallback)."""
+    if test in _libs:
+        return _libs[test]
+    path = TEST_LIB_PATH if test else LIB_PATH
+    if not path.exists():
         raise RuntimeError(
-            f"capsule_amd: HIP library {LIB_PATH} not built; run "
+            f"capsule_amd: HIP library {path} not built; run "
             "`python -c 'import __graft_entry__ as g; g.build()'` (make -C capsule_amd/csrc)")
-    L = ctypes.CDLL(str(LIB_PATH))
+    L = ctypes.CDLL(str(path))
     vp, u32, u16, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_int
     P = ctypes.POINTER
     L.cgpu_abi_version.restype = i32
@@ -159,6 +165,8 @@ def lib():
     L.cgpu_ctx_create.argtypes = [i32, P(vp)]
     L.cgpu_ctx_destroy.restype = None
     L.cgpu_ctx_destroy.argtypes = [vp]
+    L.cgpu_ctx_check.restype = i32
+    L.cgpu_ctx_check.argtypes = [vp, vp]
     L.cgpu_parse_batch.restype = i32
     L.cgpu_parse_batch.argtypes = [vp, P(Batch), u32, P(ParseOut), vp]
     L.cgpu_parse_host.restype = i32
@@ -198,8 +206,8 @@ def lib():
     L.cgpu_reconcile_frames.restype = i32
     L.cgpu_reconcile_frames.argtypes = [vp, vp, vp, vp, u32, u32, u32, vp]
     if L.cgpu_abi_version() != ABI_VERSION:
-        raise RuntimeError("capsule_amd: libcapsule_gpu.so ABI version mismatch")
-    _lib = L
+        raise RuntimeError(f"capsule_amd: {path.name} ABI version mismatch")
+    _libs[test] = L
     return L
 
 

@@ -173,13 +173,27 @@ class Channel:
         return self.q.pop(0) if self.q else []
 
 
+def _size(burst):
+    if burst is None:
+        return 0
+    return burst.n if isinstance(burst, packets.PacketBatch) else len(burst)
+
+
 class Poll(Batch):
     """`Poll::new(rx)` / `poll_fn(f)` (batch/poll.rs:47-62): `replenish`
     pulls the next burst from the receive side -- a PacketRx (anything with
     `receive()`), a function returning a burst, or an iterator of bursts.
-    A burst is a PacketBatch or a list of frames (bytes)."""
+    A burst is a PacketBatch or a list of frames (bytes).
 
-    def __init__(self, ctx, rx, device="cuda:0"):
+    `target`: packets to gather per replenish.  The reference pulls one
+    burst (at most RX_BURST_MAX = 32 mbufs, dpdk/port.rs:149-171) per
+    replenish, which is `target=1`; a device call costs a fixed ~20 us
+    (DESIGN.md §8), so the GPU seam keeps pulling until it holds `target`
+    packets or a pull brings nothing (the queue is drained: nothing waits for
+    packets that have not arrived), and runs the pulled bursts as one, in
+    arrival order."""
+
+    def __init__(self, ctx, rx, device="cuda:0", target=1):
         super().__init__(ctx)
         if hasattr(rx, "receive"):
             self.pull = rx.receive
@@ -189,15 +203,28 @@ class Poll(Batch):
             it = iter(rx)
             self.pull = lambda: next(it, None)
         self.device = device
+        self.target = max(1, int(target))
         self.pending = None
+        self.pulls = 0  # receive() calls so far
 
     def replenish(self):
-        nxt = self.pull()
-        if nxt is None or (not isinstance(nxt, packets.PacketBatch) and len(nxt) == 0):
+        parts, total = [], 0
+        while total < self.target:
+            nxt = self.pull()
+            self.pulls += 1
+            if _size(nxt) == 0:
+                break
+            parts.append(nxt)
+            total += _size(nxt)
+        if not parts:
             self.pending = None
             return
-        if not isinstance(nxt, packets.PacketBatch):
-            nxt = packets.PacketBatch.from_frames(nxt, self.device)
+        if all(not isinstance(p, packets.PacketBatch) for p in parts):
+            nxt = packets.PacketBatch.from_frames([f for p in parts for f in p], self.device)
+        else:
+            nxt = packets.PacketBatch.concat(
+                [p if isinstance(p, packets.PacketBatch) else
+                 packets.PacketBatch.from_frames(p, self.device) for p in parts])
         self.pending = Burst(nxt)
 
     def next_burst(self):

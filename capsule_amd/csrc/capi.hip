@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <dlfcn.h>
+#include <unistd.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -82,7 +83,7 @@ class DeviceGuard {
 
 struct cgpu_ctx {
   int device;
-  hipStream_t stream;  // used by the synchronous host entry points
+  hipStream_t stream = nullptr;  // used by the synchronous host entry points
   // pinned + device staging for cgpu_parse_host
   uint8_t *h_arena = nullptr, *d_arena = nullptr;
   size_t arena_cap = 0;
@@ -96,8 +97,17 @@ struct cgpu_ctx {
   size_t gb_cap = 0;              // entries
   // host regions registered for zero-copy ingress
   cgpu::HostRegion reg[cgpu::kMaxRegions];
-  bool reg_owned[cgpu::kMaxRegions];  // registered here (else: already page-locked)
+  bool reg_owned[cgpu::kMaxRegions];  // registered here (else: the caller's pinned allocation)
   uint32_t nreg = 0;
+  // the device error word (kernels.hpp kDevErrSched), and whether a call
+  // since it was last read took the wave schedule
+  uint32_t *dev_err = nullptr;
+  bool err_pending = false;
+  // cgpu_parse_frames' direct path: page-locked host memory the kernel
+  // reads its descriptors from and writes its results to (no copies)
+  uint8_t *h_io = nullptr, *d_io = nullptr;
+  size_t io_cap = 0;
+  uint32_t sched_spins = cgpu::kSchedSpins;
   // The rows kernels' wave schedules (kernels.hpp ParseArgs::sched): waves
   // resident on this device, and one granule buffer per stream the context
   // has launched on, with the tag of its latest call.  Calls on one stream
@@ -115,60 +125,111 @@ struct cgpu_ctx {
 
 namespace {
 
-// Resident waves of the rows kernels: the CU count x 32 (8 waves per SIMD),
-// or CGPU_TEST_SCHED_WAVES (test hook: a decimal 64..2^20, so that small
-// batches run several rounds of waves and take the schedule).
+// Resident waves of the rows kernels: the CU count x 32 (8 waves per SIMD).
 uint32_t resident_waves(int device) {
-  if (const char *e = getenv("CGPU_TEST_SCHED_WAVES")) {
-    char *end = nullptr;
-    const unsigned long v = strtoul(e, &end, 10);
-    if (end != e && *end == '\0' && v >= 64ul && v <= (1ul << 20)) {
-      fprintf(stderr, "capsule_gpu: test hook CGPU_TEST_SCHED_WAVES=%lu active\n", v);
-      return (uint32_t)v;
-    }
-    fprintf(stderr, "capsule_gpu: ignoring malformed CGPU_TEST_SCHED_WAVES\n");
-  }
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
     return 0;
   return (uint32_t)cus * cgpu::kResidentWavesPerCU;
 }
 
+#ifdef CGPU_TEST_HOOKS
+// Test build only (libcapsule_gpu_test.so; the product library reads no
+// environment): a decimal value of `name` within [lo, hi], else `dflt`.
+uint32_t test_hook(const char *name, uint32_t lo, uint32_t hi, uint32_t dflt) {
+  const char *e = getenv(name);
+  if (!e) return dflt;
+  char *end = nullptr;
+  const unsigned long v = strtoul(e, &end, 0);
+  if (end != e && *end == '\0' && v >= lo && v <= hi) {
+    fprintf(stderr, "capsule_gpu: test hook %s=%lu active\n", name, v);
+    return (uint32_t)v;
+  }
+  fprintf(stderr, "capsule_gpu: ignoring malformed %s\n", name);
+  return dflt;
+}
+#endif
+
+// The schedule buffer of `key` (a stream), allocated on first use and
+// zeroed on `stream`, ordered before the launch that first reads it;
+// nullptr if it cannot be had (the call then runs unordered).
+cgpu_ctx::Sched *sched_buffer(cgpu_ctx *c, unsigned long long key, hipStream_t stream) {
+  for (auto &x : c->sched)
+    if (x.key == key) return &x;
+  unsigned long long *buf = nullptr;
+  const size_t bytes = sizeof(unsigned long long) * cgpu::kSchedMax;
+  if (hipMalloc((void **)&buf, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (hipMemsetAsync(buf, 0, bytes, stream) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(buf);
+    return nullptr;
+  }
+  c->sched.push_back(cgpu_ctx::Sched{key, buf, 0u});
+  return &c->sched.back();
+}
+
+unsigned long long sched_key(void *stream) {
+  const unsigned long long sid = stream_id(stream);
+  return sid ? sid : (unsigned long long)(uintptr_t)stream | (1ull << 63);
+}
+
 // Gives a call of a.n frames on `stream` its wave schedule when the launch
 // is more than one round of waves: the last min(groups - resident,
 // kSchedMax) groups of 64 frames, rounded down to whole lists of 256, are
 // ordered longest span first (parse.hip).  The kernel ignores it unless it
-// runs the rows variant.
-int set_schedule(cgpu_ctx *c, cgpu::ParseArgs &a, void *stream) {
+// runs the rows variant.  The schedule is an optimisation, never needed for
+// a result: a stream that is being captured into a graph (replays of one
+// graph would share a buffer and a tag) or a buffer that cannot be
+// allocated leaves the call unordered.
+void set_schedule(cgpu_ctx *c, cgpu::ParseArgs &a, void *stream) {
   a.sched = nullptr;
+  a.dev_err = c->dev_err;
+  a.sched_spins = c->sched_spins;
   const uint32_t groups = (a.n + 63u) / 64u;
-  if (c->resident_waves == 0 || groups <= c->resident_waves) return 0;
+  if (c->resident_waves == 0 || groups <= c->resident_waves) return;
   // whole lists of 256 groups (one ordering workgroup each)
   const uint32_t over = groups - c->resident_waves;
   const uint32_t n_sched = (over < cgpu::kSchedMax ? over : cgpu::kSchedMax) / 256u * 256u;
-  if (n_sched == 0) return 0;
-  const unsigned long long sid = stream_id(stream);
-  const unsigned long long key = sid ? sid : (unsigned long long)(uintptr_t)stream | (1ull << 63);
-  cgpu_ctx::Sched *b = nullptr;
-  for (auto &x : c->sched)
-    if (x.key == key) b = &x;
-  if (!b) {
-    unsigned long long *buf = nullptr;
-    const size_t bytes = sizeof(unsigned long long) * cgpu::kSchedMax;
-    if (hipMalloc((void **)&buf, bytes) != hipSuccess) return CGPU_ENOMEM;
-    if (hipMemset(buf, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-      (void)hipFree(buf);
-      return CGPU_EIO;
-    }
-    c->sched.push_back(cgpu_ctx::Sched{key, buf, 0u});
-    b = &c->sched.back();
+  if (n_sched == 0) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
   }
+  if (cs != hipStreamCaptureStatusNone) return;
+  cgpu_ctx::Sched *b = sched_buffer(c, sched_key(stream), (hipStream_t)stream);
+  if (!b) return;
   if (++b->tag == 0u) b->tag = 1u;  // tags are never 0: a zeroed granule matches no call
   a.sched = b->buf;
   a.sched_n = n_sched;
   a.sched_from = groups - n_sched;
   a.sched_tag = b->tag;
-  return 0;
+  c->err_pending = true;
+}
+
+// Reads and clears the context's device error word on its stream (after
+// the caller has synchronised the streams whose calls it covers): CGPU_EIO
+// if a wave gave up on the schedule.
+int take_dev_err(cgpu_ctx *c) {
+  uint32_t w = 0;
+  if (hipMemcpyAsync(&w, c->dev_err, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return CGPU_EIO;
+  if (w == 0) return 0;
+  if (hipMemsetAsync(c->dev_err, 0, 4, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return CGPU_EIO;
+  return CGPU_EIO;
+}
+
+// The end of a synchronous entry point that ran on the context's stream.
+int sync_done(cgpu_ctx *c) {
+  if (!c->err_pending) return 0;
+  c->err_pending = false;
+  return take_dev_err(c);
 }
 
 }  // namespace
@@ -253,17 +314,48 @@ int cgpu_ctx_create(int hip_device, cgpu_ctx **out) {
   if (!c) return fail(CGPU_ENOMEM);
   c->device = hip_device;
   c->resident_waves = resident_waves(hip_device);
+#ifdef CGPU_TEST_HOOKS
+  // CGPU_TEST_SCHED_WAVES: resident waves as the schedule counts them (small
+  // batches then run several rounds and take it); CGPU_TEST_SCHED_SPINS:
+  // granule polls before a wave gives up (0: every ordered wave gives up)
+  c->resident_waves = test_hook("CGPU_TEST_SCHED_WAVES", 64u, 1u << 20, c->resident_waves);
+  c->sched_spins = test_hook("CGPU_TEST_SCHED_SPINS", 0u, cgpu::kSchedSpins, c->sched_spins);
+#endif
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(CGPU_EIO);
   }
+  // the device error word, and the schedule buffer of the context's own
+  // stream (the synchronous entry points' calls)
+  if (hipMalloc((void **)&c->dev_err, 4) != hipSuccess || hipMemsetAsync(c->dev_err, 0, 4, c->stream) != hipSuccess ||
+      (c->resident_waves && !sched_buffer(c, sched_key(c->stream), c->stream)) ||
+      hipStreamSynchronize(c->stream) != hipSuccess) {
+    (void)hipGetLastError();
+    cgpu_ctx_destroy(c);
+    return fail(CGPU_ENOMEM);
+  }
   *out = c;
+  return ok();
+}
+
+int cgpu_ctx_check(cgpu_ctx *c, void *stream) {
+  if (!c) return fail(CGPU_EINVAL);
+  DeviceGuard dg(c->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
+  if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(CGPU_EIO);
+  c->err_pending = false;
+  if (int e = take_dev_err(c)) return fail(e);
   return ok();
 }
 
 void cgpu_ctx_destroy(cgpu_ctx *c) {
   if (!c) return;
   DeviceGuard dg(c->device);
+  // nothing is freed or unpinned under a call still running on the
+  // context's stream (the synchronous entry points' stream)
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->dev_err) (void)hipFree(c->dev_err);
+  if (c->h_io) (void)hipHostFree(c->h_io);
   if (c->h_arena) (void)hipHostFree(c->h_arena);
   if (c->d_arena) (void)hipFree(c->d_arena);
   if (c->h_desc) (void)hipHostFree(c->h_desc);
@@ -274,7 +366,7 @@ void cgpu_ctx_destroy(cgpu_ctx *c) {
   if (c->d_zc) (void)hipFree(c->d_zc);
   for (uint32_t r = 0; r < c->nreg; ++r)
     if (c->reg_owned[r]) (void)hipHostUnregister((void *)(uintptr_t)c->reg[r].host_base);
-  (void)hipStreamDestroy(c->stream);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -312,7 +404,7 @@ int cgpu_parse_batch(cgpu_ctx *ctx, const cgpu_batch *batch, uint32_t flags,
   a.hash = out->flow_hash;
   a.fields = out->fields;
   a.ext = out->ext;
-  if (int e = set_schedule(ctx, a, stream)) return fail(e);
+  set_schedule(ctx, a, stream);
   hipError_t e = cgpu::launch_parse(a, flags, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e);
   return ok();
@@ -430,6 +522,7 @@ static int parse_staged(cgpu_ctx *ctx, uint32_t n, Get get, uint32_t flags, uint
                                flow_hash, fields, 0))
     return e;
   if (hipStreamSynchronize(s) != hipSuccess) return fail(CGPU_EIO);
+  if (int e = sync_done(ctx)) return fail(e);
   return ok();
 }
 
@@ -585,6 +678,7 @@ static int parse_zero_copy(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32
     bad_total += hcnt->bad;
     at += m;
   }
+  if (int e = sync_done(ctx)) return fail(e);
   return bad_total ? fail(CGPU_EINVAL) : ok();
 }
 
@@ -636,7 +730,86 @@ static int parse_frames_zero_copy(cgpu_ctx *ctx, const uint8_t *const *pkt, cons
     bad_total += hcnt->bad;
     at += m;
   }
+  if (int e = sync_done(ctx)) return fail(e);
   return bad_total ? fail(CGPU_EINVAL) : ok();
+}
+
+// Zero-copy from (frame address, length) pairs, direct: when every frame of
+// the burst lies in one registered region within a 4 GiB window, the parse
+// kernel reads the frames through the device's mapping of that window, its
+// descriptors (each frame's offset in the window, its length) from
+// page-locked host memory, and writes its results there: one launch and
+// one synchronisation per call, no copy engine and no gather.  This is the
+// latency path for bursts of the RX path's size (RX_BURST_MAX = 32 per
+// rte_eth_rx_burst, port.rs:149-171, aggregated by the caller); past
+// kDirectMax frames the gather path's full-line PCIe reads win
+// (DESIGN.md §8).  Returns 1 when the burst does not qualify (then nothing
+// ran).
+constexpr uint32_t kDirectMax = 1u << 14;
+
+static int parse_frames_direct(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *len,
+                               uint32_t n, uint32_t flags, uint32_t *meta, uint32_t *csum,
+                               uint64_t *flow_hash, cgpu_hdr_record *fields) {
+  if (n > kDirectMax) return 1;
+  // one region holds every frame
+  uint32_t r = 0;
+  const uint64_t a0 = (uint64_t)(uintptr_t)pkt[0];
+  for (; r < ctx->nreg; ++r)
+    if (a0 >= ctx->reg[r].host_base && a0 + len[0] <= ctx->reg[r].host_base + ctx->reg[r].bytes) break;
+  if (r == ctx->nreg) return 1;
+  const uint64_t rb = ctx->reg[r].host_base, re = rb + ctx->reg[r].bytes;
+  uint64_t lo = a0, hi = a0 + len[0];
+  for (uint32_t i = 1; i < n; ++i) {
+    const uint64_t a = (uint64_t)(uintptr_t)pkt[i], e = a + len[i];
+    if (a < rb || e > re) return 1;
+    lo = a < lo ? a : lo;
+    hi = e > hi ? e : hi;
+  }
+  lo &= ~(uint64_t)255u;  // a frame's alignment within the window is its own
+  if (lo < rb) lo = rb;
+  if (hi - lo > 0xffff0000ull) return 1;
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
+  const HostLayout lay(n, fields != nullptr);
+  if (lay.end > ctx->io_cap) {
+    if (ctx->h_io) (void)hipHostFree(ctx->h_io);
+    ctx->h_io = ctx->d_io = nullptr;
+    ctx->io_cap = 0;
+    const size_t cap = align_up(lay.end + lay.end / 2, 1u << 16);
+    if (hipHostMalloc((void **)&ctx->h_io, cap, hipHostMallocDefault) != hipSuccess) return fail(CGPU_ENOMEM);
+    if (hipHostGetDevicePointer((void **)&ctx->d_io, ctx->h_io, 0) != hipSuccess || !ctx->d_io) {
+      (void)hipHostFree(ctx->h_io);
+      ctx->h_io = nullptr;
+      return fail(CGPU_EIO);
+    }
+    ctx->io_cap = cap;
+  }
+  uint32_t *hoff = (uint32_t *)(ctx->h_io + lay.off);
+  for (uint32_t i = 0; i < n; ++i) hoff[i] = (uint32_t)((uint64_t)(uintptr_t)pkt[i] - lo);
+  memcpy(ctx->h_io + lay.len, len, 2ull * n);
+  uint8_t *D = ctx->d_io;
+  cgpu_batch b;
+  b.arena = (const uint8_t *)(uintptr_t)(ctx->reg[r].dev_base + (lo - rb));
+  b.arena_len = hi - lo;
+  b.off = (const uint32_t *)(D + lay.off);
+  b.len = (const uint16_t *)(D + lay.len);
+  b.n = n;
+  cgpu_parse_out o;
+  o.meta = (uint32_t *)(D + lay.meta);
+  o.csum = csum ? (uint32_t *)(D + lay.csum) : nullptr;
+  o.flow_hash = flow_hash ? (uint64_t *)(D + lay.hash) : nullptr;
+  o.fields = fields ? (cgpu_hdr_record *)(D + lay.fields) : nullptr;
+  o.ext = nullptr;
+  if (!csum) flags &= ~(CGPU_F_CSUM_IP | CGPU_F_CSUM_L4);
+  if (!flow_hash) flags &= ~CGPU_F_FLOW_HASH;
+  if (int e = cgpu_parse_batch(ctx, &b, flags, &o, ctx->stream)) return e;
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(CGPU_EIO);
+  memcpy(meta, ctx->h_io + lay.meta, 4ull * n);
+  if (csum) memcpy(csum, ctx->h_io + lay.csum, 4ull * n);
+  if (flow_hash) memcpy(flow_hash, ctx->h_io + lay.hash, 8ull * n);
+  if (fields) memcpy(fields, ctx->h_io + lay.fields, sizeof(cgpu_hdr_record) * (size_t)n);
+  if (int e = sync_done(ctx)) return fail(e);
+  return ok();
 }
 
 extern "C" {
@@ -661,22 +834,55 @@ int cgpu_parse_frames(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *
   if (!ctx) return fail(CGPU_EINVAL);
   if (n == 0) return ok();
   if (!pkt || !len || !meta) return fail(CGPU_EINVAL);
-  if (ingress == CGPU_INGRESS_ZERO_COPY)
+  if (ingress == CGPU_INGRESS_ZERO_COPY) {
+    if (ctx->nreg == 0) return fail(CGPU_EINVAL);
+    const int d = parse_frames_direct(ctx, pkt, len, n, flags, meta, csum, flow_hash, fields);
+    if (d <= 0) return d;
     return parse_frames_zero_copy(ctx, pkt, len, n, flags, meta, csum, flow_hash, fields);
+  }
   if (ingress != CGPU_INGRESS_STAGE) return fail(CGPU_EINVAL);
   return cgpu_parse_host(ctx, pkt, len, n, flags, meta, csum, flow_hash, fields);
 }
 
+// Host regions (DESIGN.md §13 "Host registration"): the library borrows
+// host memory only where it can tell that the range is the caller's for
+// the registration's lifetime.  A range must be whole pages: hipHostRegister
+// pins and maps whole pages, so a partial page would pin (and, for a
+// pageable copy's on-the-fly pinning, alias) bytes of allocations the
+// caller does not own.  Memory that is already page-locked is accepted only
+// when the whole range lies inside ONE pinned allocation (hipHostMalloc'd,
+// torch pinned memory); a range that merely overlaps someone's pinned pages
+// is refused rather than mapped through a registration whose lifetime the
+// library does not control.  Regions of one context never share a page.
 int cgpu_host_register(cgpu_ctx *ctx, void *base, size_t bytes) {
-  if (!ctx || !base || bytes == 0 || ctx->nreg >= cgpu::kMaxRegions) return fail(CGPU_EINVAL);
+  if (!ctx || !base || bytes == 0) return fail(CGPU_EINVAL);
+  static const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
+  const uint64_t lo = (uint64_t)(uintptr_t)base, hi = lo + bytes;
+  if (lo % page || bytes % page || hi < lo) return fail(CGPU_EINVAL);
+  if (ctx->nreg >= cgpu::kMaxRegions) return fail(CGPU_EINVAL);
+  for (uint32_t r = 0; r < ctx->nreg; ++r) {
+    const cgpu::HostRegion &g = ctx->reg[r];
+    if (lo < g.host_base + g.bytes && g.host_base < hi) return fail(CGPU_EINVAL);
+  }
   DeviceGuard dg(ctx->device);
   if (!dg.ok()) return fail(CGPU_ENODEV);
-  // Memory that is already page-locked (hipHostMalloc'd, or registered by
-  // someone else) is only mapped; anything else is registered here.
   hipPointerAttribute_t attr;
-  const bool locked = hipPointerGetAttributes(&attr, base) == hipSuccess &&
-                      attr.type == hipMemoryTypeHost;
+  bool locked = hipPointerGetAttributes(&attr, base) == hipSuccess && attr.type == hipMemoryTypeHost;
   (void)hipGetLastError();
+  if (!locked) {  // the last byte must not be page-locked either
+    hipPointerAttribute_t at2;
+    const bool last = hipPointerGetAttributes(&at2, (void *)(uintptr_t)(hi - 1)) == hipSuccess &&
+                      at2.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    if (last) return fail(CGPU_EINVAL);
+  } else {  // one pinned allocation holds the whole range
+    hipDeviceptr_t pb = nullptr;
+    size_t ps = 0;
+    const bool whole = hipMemGetAddressRange(&pb, &ps, base) == hipSuccess &&
+                       (uint64_t)(uintptr_t)pb <= lo && hi <= (uint64_t)(uintptr_t)pb + ps;
+    (void)hipGetLastError();
+    if (!whole) return fail(CGPU_EINVAL);
+  }
   const bool owned = !locked;
   if (owned && hipHostRegister(base, bytes, hipHostRegisterMapped) != hipSuccess) {
     (void)hipGetLastError();
@@ -684,11 +890,12 @@ int cgpu_host_register(cgpu_ctx *ctx, void *base, size_t bytes) {
   }
   void *dev = nullptr;
   if (hipHostGetDevicePointer(&dev, base, 0) != hipSuccess || !dev) {
+    (void)hipGetLastError();
     if (owned) (void)hipHostUnregister(base);
     return fail(CGPU_EIO);
   }
   cgpu::HostRegion &r = ctx->reg[ctx->nreg];
-  r.host_base = (uint64_t)(uintptr_t)base;
+  r.host_base = lo;
   r.dev_base = (uint64_t)(uintptr_t)dev;
   r.bytes = bytes;
   ctx->reg_owned[ctx->nreg] = owned;
@@ -696,12 +903,17 @@ int cgpu_host_register(cgpu_ctx *ctx, void *base, size_t bytes) {
   return ok();
 }
 
+// Every entry point that reads or writes registered memory runs on the
+// context's stream and has synchronised it before returning; the sync here
+// also covers a call that failed part-way, so no device access to the
+// region can follow its unpinning.
 int cgpu_host_unregister(cgpu_ctx *ctx, void *base) {
   if (!ctx || !base) return fail(CGPU_EINVAL);
   for (uint32_t r = 0; r < ctx->nreg; ++r) {
     if (ctx->reg[r].host_base != (uint64_t)(uintptr_t)base) continue;
     DeviceGuard dg(ctx->device);
     if (!dg.ok()) return fail(CGPU_ENODEV);
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(CGPU_EIO);
     if (ctx->reg_owned[r] && hipHostUnregister(base) != hipSuccess) return fail(CGPU_EIO);
     for (uint32_t q = r + 1; q < ctx->nreg; ++q) {
       ctx->reg[q - 1] = ctx->reg[q];
@@ -761,24 +973,13 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
     pm->dev.seed_hash = rd();
     pm->dev.seed_tag = rd();
   }
-  // Test hook: CGPU_TEST_NAT64_TAG_MASK=<hex> keeps only those bits of the
-  // claim tags, so distinct keys collide on them and the tail's repair runs
-  // (every batch then takes the serial repair: slow, never wrong).  A value
-  // that is not a nonzero hex mask is ignored; an active hook says so once.
   pm->dev.tag_mask = 0xffffffffu;
-  if (const char *tm = getenv("CGPU_TEST_NAT64_TAG_MASK")) {
-    char *end = nullptr;
-    const unsigned long v = strtoul(tm, &end, 16);
-    if (end != tm && *end == '\0' && (v & 0xffffffffu) != 0u) {
-      pm->dev.tag_mask = (uint32_t)v;
-      static bool said = false;
-      if (!said) {
-        said = true;
-        fprintf(stderr, "capsule_gpu: test hook CGPU_TEST_NAT64_TAG_MASK=%08x active (claim tags masked)\n",
-                pm->dev.tag_mask);
-      }
-    }
-  }
+#ifdef CGPU_TEST_HOOKS
+  // CGPU_TEST_NAT64_TAG_MASK: keep only these bits of the claim tags, so
+  // that distinct keys collide on them and the tail's repair runs (every
+  // batch then takes the serial repair: slow, never wrong)
+  pm->dev.tag_mask = test_hook("CGPU_TEST_NAT64_TAG_MASK", 1u, 0xffffffffu, 0xffffffffu);
+#endif
   if (hipEventCreateWithFlags(&pm->done, hipEventDisableTiming) != hipSuccess) {
     (void)hipFree(mem);
     delete pm;
@@ -1175,7 +1376,7 @@ int cgpu_reconcile(cgpu_ctx *ctx, uint8_t *arena, uint64_t arena_len, const uint
   a.meta_in = meta;
   a.depth = depth;
   a.rstatus = status;
-  if (int e = set_schedule(ctx, a, stream)) return fail(e);
+  set_schedule(ctx, a, stream);
   hipError_t e = cgpu::launch_reconcile(a, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e);
   return ok();
@@ -1262,7 +1463,7 @@ int cgpu_reconcile_frames(cgpu_ctx *ctx, uint8_t *const *frames, const uint16_t 
     a.meta_in = (const uint32_t *)(D + o_meta);
     a.depth = depth;
     a.rstatus = D + o_st;
-    if (int e = set_schedule(ctx, a, s)) return fail(e);
+    set_schedule(ctx, a, s);
     hipError_t e = cgpu::launch_reconcile(a, s);
     if (e != hipSuccess) return hip_fail(e);
     if (hipMemcpyAsync(H + o_st, D + o_st, m, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1274,6 +1475,7 @@ int cgpu_reconcile_frames(cgpu_ctx *ctx, uint8_t *const *frames, const uint16_t 
         if (region[i] == r) status[i] = H[o_st + q++];
     }
   }
+  if (int e = sync_done(ctx)) return fail(e);
   return ok();
 }
 

@@ -38,12 +38,24 @@ struct ParseArgs {
   unsigned long long *sched = nullptr;
   uint32_t sched_from = 0, sched_n = 0;
   uint32_t sched_tag = 0;  // this call's granule tag (never 0)
+  // A wave that polled its granule sched_spins times without seeing the tag
+  // gives up, takes no group and ORs CGPU_DEVERR_SCHED into *dev_err (the
+  // context's device error word, which cgpu_ctx_check and the synchronous
+  // entry points report as CGPU_EIO).
+  uint32_t sched_spins = 0;
+  uint32_t *dev_err = nullptr;
 };
 
 // Waves the rows kernels keep resident per CU (8 waves per SIMD), and the
 // most waves one launch orders (the granules of one schedule buffer).
 constexpr uint32_t kResidentWavesPerCU = 32;
 constexpr uint32_t kSchedMax = 8192;
+// Granule polls before a wave gives up (each poll sleeps ~0.5 us: seconds,
+// against the microseconds the ordering workgroups take; DESIGN.md §3.1
+// "Forward progress").
+constexpr uint32_t kSchedSpins = 1u << 24;
+// Bits of the context's device error word.
+constexpr uint32_t kDevErrSched = 1u;
 
 hipError_t launch_parse(const ParseArgs &a, uint32_t flags, hipStream_t s);
 // Packet::reconcile_all at a.depth (accept set in a.accept).

@@ -397,13 +397,13 @@ __device__ __forceinline__ void stream_prologue(rsrc_t rs, uint32_t base, uint32
 // lane with sc1 loads, so no fence orders anything (the R2 granule of
 // cdna_hip_programming.md Guideline 16).  The tag is the call's own (the host
 // counts calls per buffer), and the wave that takes a granule clears it, so
-// an entry an earlier launch left never matches, even one replayed from a
-// captured graph with the same tag.
+// an entry an earlier launch left never matches.  Calls captured into a
+// graph run without the schedule (capi.hip set_schedule): replays of one
+// graph would share a buffer and a tag.
 // Which wave takes which group changes no output: every frame's results are
 // its own.
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 constexpr uint32_t kSchedClasses = 64;
-constexpr uint32_t kSpinMax = 1u << 24;  // granule polls before a wave gives up (seconds)
 
 __device__ __forceinline__ uint32_t span_class(uint32_t span) {
   // quarter octaves, longest first: class 0 holds spans of 16 MiB and more,
@@ -469,7 +469,15 @@ __device__ void schedule_waves(const ParseArgs &a, uint32_t *L) {
 }
 
 // The group of 64 frames this wave takes (wave-uniform); ~0u: none (a wave
-// that gave up waiting for its granule).
+// that gave up waiting for its granule).  A give-up is never silent: the
+// wave ORs kDevErrSched into the context's device error word, and the call
+// (or the next cgpu_ctx_check) fails with CGPU_EIO.  Forward progress
+// (DESIGN.md §3.1): the ordering workgroups are the launch's lowest
+// workgroup ids and wait on nothing; each XCD places its workgroups in id
+// order, so no wave of this launch can take the slot an ordering workgroup
+// of its own XCD is waiting for.  A kernel of another stream that fills an
+// XCD delays that XCD's ordering workgroup until its own waves end; it
+// cannot block it.
 __device__ __forceinline__ uint32_t wave_group(const ParseArgs &a) {
   if (a.sched == nullptr) return blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6);
   const uint32_t v = (blockIdx.x - a.sched_n / kBlock) * (kBlock / 64u) + (threadIdx.x >> 6);
@@ -477,18 +485,19 @@ __device__ __forceinline__ uint32_t wave_group(const ParseArgs &a) {
   if (v < a.sched_from || q >= a.sched_n) return v;
   uint32_t g = ~0u;
   if ((threadIdx.x & 63u) == 0u) {
-    for (uint32_t spins = 0; spins < kSpinMax; ++spins) {
+    for (uint32_t spins = 0; spins < a.sched_spins; ++spins) {
       const unsigned long long x = __hip_atomic_load((gu64 *)(a.sched + q), __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT);
       if ((uint32_t)(x >> 32) == a.sched_tag) {
         g = (uint32_t)x;
-        // consumed: cleared for the next launch, so that a launch replayed
-        // with the same tag (a captured graph) never reads this one's entry
+        // consumed: cleared for the next launch, so that no later launch
+        // can read this one's entry
         __hip_atomic_store((gu64 *)(a.sched + q), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       __builtin_amdgcn_s_sleep(8);
     }
+    if (g == ~0u) __hip_atomic_fetch_or(a.dev_err, kDevErrSched, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   return (uint32_t)__shfl((int)g, 0);
 }

@@ -44,20 +44,29 @@ def _stream_handle(stream):
 class Context:
     """`cgpu_ctx`: one per core thread / RX queue (runtime/core_map.rs:236-293)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, test_hooks=False):
         if not torch.cuda.is_available():
             raise RuntimeError("capsule_amd: no HIP device visible")
         self.device = torch.device("cuda", device)
+        # test_hooks=True: a context of the test build (tests only), whose
+        # objects all go through that library
+        self.L = N.lib(test=test_hooks)
         self._h = ctypes.c_void_p()
-        N.check(N.lib().cgpu_ctx_create(device, ctypes.byref(self._h)), "cgpu_ctx_create")
+        N.check(self.L.cgpu_ctx_create(device, ctypes.byref(self._h)), "cgpu_ctx_create")
 
     @property
     def handle(self):
         return self._h
 
+    def check(self, stream=None):
+        """`cgpu_ctx_check`: synchronise `stream` (torch's current one by
+        default) and raise CgpuError(EIO) if a kernel of this context set the
+        device error word since the last check."""
+        N.check(self.L.cgpu_ctx_check(self._h, _stream_handle(stream)), "cgpu_ctx_check")
+
     def close(self):
         if self._h:
-            N.lib().cgpu_ctx_destroy(self._h)
+            self.L.cgpu_ctx_destroy(self._h)
             self._h = ctypes.c_void_p()
 
     def __del__(self):
@@ -93,6 +102,24 @@ class PacketBatch:
         from .synth import pack_frames
 
         return cls.from_numpy(*pack_frames(frames, slot), device)
+
+    @classmethod
+    def concat(cls, parts):
+        """Bursts laid end to end (arenas concatenated, offsets moved), in
+        order: the device image of the mbufs of several RX bursts."""
+        if len(parts) == 1:
+            return parts[0]
+        arenas, offs, base = [], [], 0
+        for p in parts:
+            arenas.append(p.arena)
+            o = p.off.to(torch.int64) & 0xFFFFFFFF
+            offs.append(o + base)
+            base += p.arena.numel()
+        if base > 0xFFFF0000:
+            raise ValueError("concatenated arena past 4 GiB")
+        off = torch.cat(offs)
+        off = torch.where(off >= 1 << 31, off - (1 << 32), off).to(torch.int32)
+        return cls(torch.cat(arenas), off, torch.cat([p.len for p in parts]))
 
     def cbatch(self):
         b = N.Batch()
@@ -191,7 +218,7 @@ def parse(ctx, batch, flags=None, fields=False, out=None, stream=None, ext=False
     po.fields = out.fields.data_ptr() if (fields and out.fields is not None) else None
     po.ext = out.ext.data_ptr() if (ext and out.ext is not None) else None
     cb = batch.cbatch()
-    rc = N.lib().cgpu_parse_batch(ctx.handle, ctypes.byref(cb), flags, ctypes.byref(po),
+    rc = ctx.L.cgpu_parse_batch(ctx.handle, ctypes.byref(cb), flags, ctypes.byref(po),
                                   _stream_handle(stream))
     N.check(rc, "cgpu_parse_batch")
     return ParsedBatch(out.meta[:n], out.csum[:n] if out.csum is not None else None,
@@ -212,7 +239,7 @@ def parse_host(ctx, frames, flags=None, fields=False):
     csum = np.zeros(n, np.uint32)
     fh = np.zeros(n, np.uint64)
     fl = np.zeros((n, N.HDR_RECORD_SIZE), np.uint8) if fields else None
-    rc = N.lib().cgpu_parse_host(
+    rc = ctx.L.cgpu_parse_host(
         ctx.handle, ptrs, lens.ctypes.data, n, flags, meta.ctypes.data, csum.ctypes.data,
         fh.ctypes.data, fl.ctypes.data if fields else None)
     N.check(rc, "cgpu_parse_host")
@@ -222,16 +249,40 @@ def parse_host(ctx, frames, flags=None, fields=False):
 
 class HostRegion:
     """A host memory range registered for zero-copy ingress (a mempool's
-    memzone); unregistered on close()."""
+    memzone): whole pages (cgpu_host_register refuses anything else).
+    Unregistered on close(), on leaving a `with` block, or when collected;
+    the caller keeps the memory mapped until then (`mem`, if given, is held
+    here so that it cannot be freed first)."""
 
-    def __init__(self, ctx, base, nbytes):
-        self.ctx, self.base = ctx, base
-        N.check(N.lib().cgpu_host_register(ctx.handle, base, nbytes), "cgpu_host_register")
+    def __init__(self, ctx, base, nbytes, mem=None):
+        self.ctx, self.base, self.nbytes, self._mem = ctx, None, nbytes, mem
+        N.check(ctx.L.cgpu_host_register(ctx.handle, base, nbytes), "cgpu_host_register")
+        self.base = base
+
+    @classmethod
+    def of(cls, ctx, mem):
+        """Register a numpy u8 array of whole pages (synth.host_buffer,
+        synth.pinned_buffer) and keep it alive with the registration."""
+        return cls(ctx, mem.ctypes.data, mem.nbytes, mem=mem)
 
     def close(self):
-        if self.base is not None:
-            N.check(N.lib().cgpu_host_unregister(self.ctx.handle, self.base), "cgpu_host_unregister")
-            self.base = None
+        if self.base is not None and self.ctx.handle:
+            N.check(self.ctx.L.cgpu_host_unregister(self.ctx.handle, self.base),
+                    "cgpu_host_unregister")
+        self.base = None
+        self._mem = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def parse_mbufs(ctx, mbufs, flags=None, ingress=N.INGRESS_STAGE, fields=False):
@@ -247,7 +298,7 @@ def parse_mbufs(ctx, mbufs, flags=None, ingress=N.INGRESS_STAGE, fields=False):
     csum = np.zeros(n, np.uint32)
     fh = np.zeros(n, np.uint64)
     fl = np.zeros((n, N.HDR_RECORD_SIZE), np.uint8) if fields else None
-    rc = N.lib().cgpu_parse_mbufs(
+    rc = ctx.L.cgpu_parse_mbufs(
         ctx.handle, mbufs.ctypes.data, n, flags, ingress, meta.ctypes.data, csum.ctypes.data,
         fh.ctypes.data, fl.ctypes.data if fields else None)
     N.check(rc, "cgpu_parse_mbufs")
@@ -268,7 +319,7 @@ def parse_frames(ctx, addrs, lens, flags=None, ingress=N.INGRESS_STAGE, fields=F
     csum = np.zeros(n, np.uint32)
     fh = np.zeros(n, np.uint64)
     fl = np.zeros((n, N.HDR_RECORD_SIZE), np.uint8) if fields else None
-    rc = N.lib().cgpu_parse_frames(
+    rc = ctx.L.cgpu_parse_frames(
         ctx.handle, addrs.ctypes.data, lens.ctypes.data, n, flags, ingress, meta.ctypes.data,
         csum.ctypes.data, fh.ctypes.data, fl.ctypes.data if fields else None)
     N.check(rc, "cgpu_parse_frames")
@@ -318,7 +369,7 @@ def group_by(ctx, key, n_groups=None, by="key", idx=None, stream=None):
     if idx is None:
         idx = torch.empty(n, dtype=torch.int32, device=key.device)
     off = torch.empty(n_groups + 1, dtype=torch.int32, device=key.device)
-    rc = N.lib().cgpu_group_by(ctx.handle, _ptr(key.contiguous()), kind, n, n_groups, _ptr(idx),
+    rc = ctx.L.cgpu_group_by(ctx.handle, _ptr(key.contiguous()), kind, n, n_groups, _ptr(idx),
                                _ptr(off), _stream_handle(stream))
     N.check(rc, "cgpu_group_by")
     return Groups(idx[:n], off)
@@ -369,7 +420,7 @@ def set_ip(ctx, batch, meta, src=None, dst=None, stream=None, status=None):
     d, ds = _addr_tensor(dst, n, dev)
     if status is None:
         status = torch.empty(n, dtype=torch.uint8, device=dev)
-    rc = N.lib().cgpu_set_ip(ctx.handle, _ptr(batch.arena), batch.arena.numel(), _ptr(batch.off),
+    rc = ctx.L.cgpu_set_ip(ctx.handle, _ptr(batch.arena), batch.arena.numel(), _ptr(batch.off),
                              _ptr(batch.len), _ptr(meta), n, _ptr(s), ss, _ptr(d), ds,
                              _ptr(status), _stream_handle(stream))
     N.check(rc, "cgpu_set_ip")
@@ -400,7 +451,7 @@ def reconcile(ctx, batch, meta, flags=None, depth="l4", stream=None, status=None
         flags = parse_flags()
     if status is None:
         status = torch.empty(n, dtype=torch.uint8, device=dev)
-    rc = N.lib().cgpu_reconcile(ctx.handle, _ptr(batch.arena), batch.arena.numel(), _ptr(batch.off),
+    rc = ctx.L.cgpu_reconcile(ctx.handle, _ptr(batch.arena), batch.arena.numel(), _ptr(batch.off),
                                 _ptr(batch.len), _ptr(meta), n, flags, _DEPTH[depth], _ptr(status),
                                 _stream_handle(stream))
     N.check(rc, "cgpu_reconcile")
@@ -421,7 +472,7 @@ def reconcile_frames(ctx, addrs, lens, meta, flags=None, depth="l4"):
     if len(lens) != n or len(meta) != n:
         raise ValueError("addrs, lens and meta must have one entry per frame")
     st = np.zeros(n, np.uint8)
-    rc = N.lib().cgpu_reconcile_frames(ctx.handle, addrs.ctypes.data, lens.ctypes.data,
+    rc = ctx.L.cgpu_reconcile_frames(ctx.handle, addrs.ctypes.data, lens.ctypes.data,
                                        meta.ctypes.data, n, flags, _DEPTH[depth], st.ctypes.data)
     N.check(rc, "cgpu_reconcile_frames")
     return st
@@ -432,7 +483,7 @@ class ReconcileLauncher:
 
     def __init__(self, ctx, batch, meta, flags, depth="l4", stream=None, status=None):
         self._keep = (batch, meta, status)
-        self._fn = N.lib().cgpu_reconcile
+        self._fn = ctx.L.cgpu_reconcile
         self._args = [ctx.handle, _ptr(batch.arena), batch.arena.numel(), _ptr(batch.off),
                       _ptr(batch.len), _ptr(meta), batch.n, flags, _DEPTH[depth], _ptr(status),
                       _stream_handle(stream)]
@@ -455,22 +506,22 @@ class Nat64Gateway:
     def __init__(self, ctx, capacity_log2=20, first_port=1025):
         self.ctx = ctx
         self._h = ctypes.c_void_p()
-        N.check(N.lib().cgpu_portmap_create(ctx.handle, capacity_log2, first_port,
+        N.check(self.ctx.L.cgpu_portmap_create(ctx.handle, capacity_log2, first_port,
                                             ctypes.byref(self._h)), "cgpu_portmap_create")
 
     def next_port(self):
         v = ctypes.c_uint16()
-        N.check(N.lib().cgpu_portmap_next_port(self._h, ctypes.byref(v)), "next_port")
+        N.check(self.ctx.L.cgpu_portmap_next_port(self._h, ctypes.byref(v)), "next_port")
         return v.value
 
     def size(self):
         v = ctypes.c_uint32()
-        N.check(N.lib().cgpu_portmap_size(self._h, ctypes.byref(v)), "size")
+        N.check(self.ctx.L.cgpu_portmap_size(self._h, ctypes.byref(v)), "size")
         return v.value
 
     def reset(self, first_port=1025, stream=None):
         """Empty the map (as a fresh gateway), asynchronously on `stream`."""
-        N.check(N.lib().cgpu_portmap_reset(self._h, first_port, _stream_handle(stream)),
+        N.check(self.ctx.L.cgpu_portmap_reset(self._h, first_port, _stream_handle(stream)),
                 "cgpu_portmap_reset")
 
     def _call(self, fn, what, grow, batch, out_arena, out_off, stream, out):
@@ -501,13 +552,13 @@ class Nat64Gateway:
         arena of the same size); out_len[i] is the new data_len for ACT
         packets and 0 otherwise.
         """
-        return self._call(N.lib().cgpu_nat64_6to4, "cgpu_nat64_6to4", 0, batch, out_arena,
+        return self._call(self.ctx.L.cgpu_nat64_6to4, "cgpu_nat64_6to4", 0, batch, out_arena,
                           out_off, stream, out)
 
     def nat_4to6(self, batch, out_arena, out_off, stream=None, out=None):
         """`nat_4to6` (examples/nat64/main.rs:86-118): output frames are 20 B
         longer, so out_off[i] must leave room for len[i] + 20 bytes."""
-        return self._call(N.lib().cgpu_nat64_4to6, "cgpu_nat64_4to6", 20, batch, out_arena,
+        return self._call(self.ctx.L.cgpu_nat64_4to6, "cgpu_nat64_4to6", 20, batch, out_arena,
                           out_off, stream, out)
 
     def nat_mbufs(self, mbufs, direction="6to4"):
@@ -521,7 +572,7 @@ class Nat64Gateway:
         disp = np.zeros(n, np.uint8)
         st = np.zeros(n, np.uint8)
         d = {"6to4": N.NAT64_6TO4, "4to6": N.NAT64_4TO6}[direction]
-        rc = N.lib().cgpu_nat64_mbufs(self.ctx.handle, self._h, d, mbufs.ctypes.data, n,
+        rc = self.ctx.L.cgpu_nat64_mbufs(self.ctx.handle, self._h, d, mbufs.ctypes.data, n,
                                       disp.ctypes.data, st.ctypes.data)
         N.check(rc, "cgpu_nat64_mbufs")
         return disp, st
@@ -540,7 +591,7 @@ class Nat64Gateway:
         disp = np.zeros(n, np.uint8)
         st = np.zeros(n, np.uint8)
         d = {"6to4": N.NAT64_6TO4, "4to6": N.NAT64_4TO6}[direction]
-        rc = N.lib().cgpu_nat64_frames(self.ctx.handle, self._h, d, addrs.ctypes.data,
+        rc = self.ctx.L.cgpu_nat64_frames(self.ctx.handle, self._h, d, addrs.ctypes.data,
                                        lens.ctypes.data, tr.ctypes.data if tr is not None else None,
                                        n, olen.ctypes.data, disp.ctypes.data, st.ctypes.data)
         N.check(rc, "cgpu_nat64_frames")
@@ -548,7 +599,7 @@ class Nat64Gateway:
 
     def close(self):
         if self._h:
-            N.lib().cgpu_portmap_destroy(self._h)
+            self.ctx.L.cgpu_portmap_destroy(self._h)
             self._h = ctypes.c_void_p()
 
     def __del__(self):
@@ -565,7 +616,7 @@ class ParseLauncher:
 
     def __init__(self, ctx, batch, out, flags, stream=None):
         self._keep = (batch, out)
-        self._fn = N.lib().cgpu_parse_batch
+        self._fn = ctx.L.cgpu_parse_batch
         self._args = [ctx.handle, None, flags, None, _stream_handle(stream)]
         self._cb = batch.cbatch()
         self._po = N.ParseOut()
@@ -591,7 +642,7 @@ class Nat64Launcher:
         self._keep = (gw, batch, out)
         self._cb = batch.cbatch()
         self._name = {"6to4": "cgpu_nat64_6to4", "4to6": "cgpu_nat64_4to6"}[direction]
-        self._fn = getattr(N.lib(), self._name)
+        self._fn = getattr(gw.ctx.L, self._name)
         self._args = [gw.ctx.handle, gw._h, ctypes.byref(self._cb), _ptr(out_arena),
                       out_arena.numel(), _ptr(out_off), _ptr(out_len), _ptr(disp), _ptr(status),
                       _stream_handle(stream)]

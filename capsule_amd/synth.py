@@ -386,17 +386,30 @@ def nat64_replies(out_arena, off, out_len):
 
 
 def host_buffer(nbytes):
-    """A zeroed u8 array of its own pages (an anonymous mmap, page-aligned,
-    sharing no page with any other allocation), for host memory that gets
-    registered with the GPU (hipHostRegister pins whole pages: a malloc'd
-    array would pin, and after unregistering leave, pages that the Python
-    heap shares with later allocations -- torch copies' host buffers among
-    them).  The mapping lives as long as the array."""
+    """A zeroed u8 array of whole pages of its own (an anonymous mmap, at
+    least `nbytes`, rounded up to the page size), for host memory that gets
+    registered with the GPU: cgpu_host_register takes whole pages only
+    (hipHostRegister pins whole pages: a malloc'd array would pin pages the
+    Python heap shares with other allocations).  The mapping lives as long
+    as the array."""
     import mmap
 
-    size = max(int(nbytes), 1)
-    m = mmap.mmap(-1, (size + mmap.PAGESIZE - 1) // mmap.PAGESIZE * mmap.PAGESIZE)
-    return np.frombuffer(m, dtype=np.uint8, count=size)
+    size = (max(int(nbytes), 1) + mmap.PAGESIZE - 1) // mmap.PAGESIZE * mmap.PAGESIZE
+    return np.frombuffer(mmap.mmap(-1, size), dtype=np.uint8)
+
+
+def pinned_buffer(nbytes):
+    """(torch pinned tensor, its u8 numpy view): page-locked host memory of
+    whole pages (at least `nbytes`), one pinned allocation, as
+    cgpu_host_register maps it without registering it again."""
+    import mmap
+
+    import torch
+
+    size = (max(int(nbytes), 1) + mmap.PAGESIZE - 1) // mmap.PAGESIZE * mmap.PAGESIZE
+    t = torch.zeros(size, dtype=torch.uint8, pin_memory=True)
+    assert t.data_ptr() % mmap.PAGESIZE == 0, "pinned allocation not page-aligned"
+    return t, t.numpy()
 
 
 def mbuf_pool(arena, off, length, mem=None, headroom=128, seed=7, room=None):

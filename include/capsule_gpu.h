@@ -41,8 +41,11 @@ extern "C" {
  *      be rewritten into lies in a registered region.
  *   4  cgpu_reconcile (Packet::reconcile_all over a parsed batch).
  *   5  cgpu_reconcile_frames (the same over frames in registered host
- *      memory, in place: the mbuf seam of a reconcile combinator).          */
-#define CGPU_ABI_VERSION 5
+ *      memory, in place: the mbuf seam of a reconcile combinator).
+ *   6  cgpu_ctx_check (the context's device error word); cgpu_host_register
+ *      takes whole pages only and refuses ranges it cannot prove are the
+ *      caller's; calls captured into a graph run without the wave order.   */
+#define CGPU_ABI_VERSION 6
 
 /* ---- call-level return codes (negative errno style) -------------------- */
 #define CGPU_OK 0
@@ -229,7 +232,20 @@ typedef struct cgpu_ctx cgpu_ctx;
  * 236-293: shared-nothing).  Contexts are independent; the library keeps
  * no global locks on the launch path.                                     */
 int cgpu_ctx_create(int hip_device, cgpu_ctx **out);
+/* Waits for the context's own stream, then frees everything the context
+ * holds and unregisters its host regions.                                 */
 void cgpu_ctx_destroy(cgpu_ctx *ctx);
+
+/* The context's device error word: kernels that cannot complete their part
+ * of a call set it instead of failing silently (today: a wave of the
+ * longest-span-first order that gave up waiting for its group, which leaves
+ * that group's 64 outputs unwritten).  Synchronises `stream`, then returns
+ * CGPU_EIO if the word was set by any call of this context since it was
+ * last read (and clears it), else 0.  The synchronous entry points read it
+ * themselves and fail with CGPU_EIO; asynchronous callers (cgpu_parse_batch,
+ * cgpu_reconcile) call this where they synchronise, as a CUDA caller checks
+ * a sticky error.                                                          */
+int cgpu_ctx_check(cgpu_ctx *ctx, void *stream);
 
 /* Batched Ethernet -> IPv4/IPv6 -> UDP/TCP parse + checksum + flow hash.
  * Replaces the per-packet chain Mbuf::parse::<Ethernet>() (ethernet.rs:279)
@@ -240,10 +256,11 @@ void cgpu_ctx_destroy(cgpu_ctx *ctx);
  * Asynchronous on `stream`.  A batch of more than one round of waves (64
  * frames a wave, 32 waves resident per CU) with checksums over long frames
  * orders its last waves longest span first through a 64 KB buffer the
- * context keeps per stream; the first such call on a stream allocates it
- * and synchronises the device once (so it must come before a graph capture
- * on that stream; captured calls replay correctly).  The results do not
- * depend on the order.                                                    */
+ * context keeps per stream (allocated by the first such call on a stream
+ * and zeroed on that stream; no device-wide synchronisation).  A call made
+ * while its stream is being captured into a graph runs without the order
+ * (replays would share the buffer), as does one whose buffer cannot be
+ * allocated.  The results do not depend on the order.                    */
 int cgpu_parse_batch(cgpu_ctx *ctx, const cgpu_batch *batch, uint32_t flags,
                      const cgpu_parse_out *out, void *stream);
 
@@ -281,7 +298,19 @@ int cgpu_parse_host(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *le
 #define CGPU_INGRESS_ZERO_COPY 1u
 
 /* Page-lock and map host memory [base, base + bytes) for the device (the
- * mempool of mempool.rs:64-106); up to 16 regions per context.             */
+ * mempool of mempool.rs:64-106); up to 16 regions per context.
+ * base and bytes must be multiples of the page size (a DPDK memzone always
+ * is), and no two regions of a context may overlap; otherwise CGPU_EINVAL.
+ * Pageable memory is registered (hipHostRegister) and unregistered again by
+ * cgpu_host_unregister / cgpu_ctx_destroy.  Memory that is already
+ * page-locked is only mapped, and only if the whole range lies inside one
+ * pinned allocation (hipHostMalloc, torch pinned memory); a range that
+ * straddles pinned and pageable pages, or several pinned allocations, is
+ * refused.  Lifetime (the ownership rule of mbuf.rs:467-479): the caller
+ * keeps the range mapped, and a pinned allocation allocated, until the
+ * region is unregistered; the library never frees or unmaps it.
+ * cgpu_host_unregister waits for the context's stream (every call that
+ * touches registered memory runs there) before unpinning.               */
 int cgpu_host_register(cgpu_ctx *ctx, void *base, size_t bytes);
 int cgpu_host_unregister(cgpu_ctx *ctx, void *base);
 

@@ -4,8 +4,15 @@
 //!
 //! The reference pulls one packet per `Batch::next` (batch/mod.rs:122-135);
 //! the GPU path works on whole bursts, so these combinators drain their
-//! upstream burst in `replenish`, make one library call for its Act
-//! packets, and then yield the results in upstream order.  Emit / Drop /
+//! upstream in `replenish`, make one library call for its Act packets, and
+//! then yield the results in upstream order.  One upstream burst is at most
+//! RX_BURST_MAX = 32 mbufs (`PortQueue::receive`, dpdk/port.rs:149-171,
+//! through `Poll::replenish`, batch/poll.rs:47-53), and a device round trip
+//! per 32 packets costs more than the CPU parse it replaces (DESIGN.md §8:
+//! about 20 us per synchronous call), so `replenish` keeps pulling upstream
+//! bursts until it holds `target` Act packets (GPU_BURST_TARGET by default)
+//! or a pull brings nothing (the RX queue is drained: a burst never waits
+//! for packets that have not arrived).  Emit / Drop /
 //! Abort pass through unchanged, as `FilterMap::next` passes them through
 //! `Disposition::map` (filter_map.rs:73-81, mod.rs:73-86).  A failed parse
 //! aborts the packet with the reference's error string, like a failing `?`
@@ -29,10 +36,16 @@ pub struct GpuParse<B: Batch<Item = Mbuf>, T: GpuTyped> {
     batch: B,
     ctx: GpuContext,
     flags: u32,
+    target: usize,
     out: ParsedBurst,
     ready: VecDeque<Disposition<T>>,
     on_parsed: Option<Box<dyn FnMut(&T, &Parsed)>>,
 }
+
+/// Act packets a GPU combinator gathers from its upstream before one device
+/// call (the synchronous call's fixed cost against the rate
+/// of one core's CPU parse).
+pub const GPU_BURST_TARGET: usize = 2048;
 
 impl<B: Batch<Item = Mbuf>, T: GpuTyped> GpuParse<B, T> {
     /// The typed chain's accept set, with the checksums verified and the flow
@@ -45,8 +58,14 @@ impl<B: Batch<Item = Mbuf>, T: GpuTyped> GpuParse<B, T> {
 
     /// Explicit flags (T::ACCEPT is always added): e.g. no checksums.
     pub fn with_flags(batch: B, ctx: GpuContext, flags: u32) -> Self {
-        GpuParse { batch, ctx, flags: flags | T::ACCEPT, out: ParsedBurst::default(),
-                   ready: VecDeque::new(), on_parsed: None }
+        GpuParse { batch, ctx, flags: flags | T::ACCEPT, target: GPU_BURST_TARGET,
+                   out: ParsedBurst::default(), ready: VecDeque::new(), on_parsed: None }
+    }
+
+    /// Act packets gathered per device call (1: one call per upstream burst).
+    pub fn with_target(mut self, target: usize) -> Self {
+        self.target = target.max(1);
+        self
     }
 
     /// Called with each Act packet and its device results as it is yielded.
@@ -56,18 +75,29 @@ impl<B: Batch<Item = Mbuf>, T: GpuTyped> GpuParse<B, T> {
     }
 }
 
-/// Drains the upstream burst: Act mbufs in one vector (in order), the other
-/// dispositions kept in their places (None marks an Act slot).
-fn drain_burst<B: Batch>(batch: &mut B) -> (Vec<Option<Disposition<B::Item>>>, Vec<B::Item>) {
+/// Drains upstream bursts until `target` Act packets are in hand or a
+/// replenish brings nothing: Act items in one vector (in order), the other
+/// dispositions kept in their places (None marks an Act slot).  Every
+/// upstream burst is drained to its end before the next replenish, so no
+/// packet is lost (`Poll::replenish` replaces its queue, poll.rs:47-53).
+fn drain_bursts<B: Batch>(batch: &mut B, target: usize)
+                          -> (Vec<Option<Disposition<B::Item>>>, Vec<B::Item>) {
     let mut slots = Vec::new();
     let mut act = Vec::new();
-    while let Some(d) = batch.next() {
-        match d {
-            Disposition::Act(p) => {
-                slots.push(None);
-                act.push(p);
+    loop {
+        batch.replenish();
+        let before = slots.len();
+        while let Some(d) = batch.next() {
+            match d {
+                Disposition::Act(p) => {
+                    slots.push(None);
+                    act.push(p);
+                }
+                other => slots.push(Some(other)),
             }
-            other => slots.push(Some(other)),
+        }
+        if act.len() >= target || slots.len() == before {
+            break;
         }
     }
     (slots, act)
@@ -77,10 +107,11 @@ impl<B: Batch<Item = Mbuf>, T: GpuTyped> Batch for GpuParse<B, T> {
     type Item = T;
 
     fn replenish(&mut self) {
-        self.batch.replenish();
-        let (slots, act) = drain_burst(&mut self.batch);
-        let (act, rc) = if act.is_empty() { (act, Ok(())) } else {
-            self.ctx.parse_burst(act, self.flags, &mut self.out)
+        let (slots, act) = drain_bursts(&mut self.batch, self.target);
+        // (data_address, data_len) pairs: the device reads the frames alone,
+        // in one launch for bursts of this size (cgpu_parse_frames' direct path)
+        let rc = if act.is_empty() { Ok(()) } else {
+            self.ctx.parse_burst_frames(&act, self.flags, &mut self.out)
         };
         let mut act = act.into_iter().enumerate();
         for s in slots {
@@ -127,12 +158,19 @@ impl<B: Batch<Item = Mbuf>, T: GpuTyped> Batch for GpuParse<B, T> {
 pub struct GpuReconcile<B: Batch<Item = T>, T: GpuTyped> {
     batch: B,
     ctx: GpuContext,
+    target: usize,
     ready: VecDeque<Disposition<T>>,
 }
 
 impl<B: Batch<Item = T>, T: GpuTyped> GpuReconcile<B, T> {
     pub fn new(batch: B, ctx: GpuContext) -> Self {
-        GpuReconcile { batch, ctx, ready: VecDeque::new() }
+        GpuReconcile { batch, ctx, target: GPU_BURST_TARGET, ready: VecDeque::new() }
+    }
+
+    /// Act packets gathered per device call.
+    pub fn with_target(mut self, target: usize) -> Self {
+        self.target = target.max(1);
+        self
     }
 }
 
@@ -140,8 +178,7 @@ impl<B: Batch<Item = T>, T: GpuTyped> Batch for GpuReconcile<B, T> {
     type Item = T;
 
     fn replenish(&mut self) {
-        self.batch.replenish();
-        let (slots, act) = drain_burst(&mut self.batch);
+        let (slots, act) = drain_bursts(&mut self.batch, self.target);
         let rc = if act.is_empty() { Ok(Vec::new()) } else { self.ctx.reconcile_typed(&act) };
         let mut act = act.into_iter().enumerate();
         for s in slots {
@@ -198,12 +235,19 @@ pub struct GpuNat64Map<B: Batch<Item = Mbuf>> {
     ctx: GpuContext,
     nat: GpuNat64,
     direction: u32,
+    target: usize,
     ready: VecDeque<Disposition<Mbuf>>,
 }
 
 impl<B: Batch<Item = Mbuf>> GpuNat64Map<B> {
     pub fn new(batch: B, ctx: GpuContext, nat: GpuNat64, direction: u32) -> Self {
-        GpuNat64Map { batch, ctx, nat, direction, ready: VecDeque::new() }
+        GpuNat64Map { batch, ctx, nat, direction, target: GPU_BURST_TARGET, ready: VecDeque::new() }
+    }
+
+    /// Act packets gathered per device call.
+    pub fn with_target(mut self, target: usize) -> Self {
+        self.target = target.max(1);
+        self
     }
 }
 
@@ -211,18 +255,7 @@ impl<B: Batch<Item = Mbuf>> Batch for GpuNat64Map<B> {
     type Item = Mbuf;
 
     fn replenish(&mut self) {
-        self.batch.replenish();
-        let mut slots: Vec<Option<Disposition<Mbuf>>> = Vec::new();
-        let mut act: Vec<Mbuf> = Vec::new();
-        while let Some(d) = self.batch.next() {
-            match d {
-                Disposition::Act(m) => {
-                    slots.push(None);
-                    act.push(m);
-                }
-                other => slots.push(Some(other)),
-            }
-        }
+        let (slots, act) = drain_bursts(&mut self.batch, self.target);
         let (done, rc) = if act.is_empty() { (Vec::new(), Ok(())) } else {
             self.nat.nat_burst(&mut self.ctx, self.direction, act)
         };

@@ -57,6 +57,7 @@ _Static_assert(CGPU_MAX_BATCH * 4ull <= 0xffffffffull, "off[] fits a 32-bit rang
 typedef void (*any_fn)(void);
 static int (*const p_ctx_create)(int, cgpu_ctx **) = cgpu_ctx_create;
 static void (*const p_ctx_destroy)(cgpu_ctx *) = cgpu_ctx_destroy;
+static int (*const p_ctx_check)(cgpu_ctx *, void *) = cgpu_ctx_check;
 static int (*const p_parse_batch)(cgpu_ctx *, const cgpu_batch *, uint32_t,
                                   const cgpu_parse_out *, void *) = cgpu_parse_batch;
 static int (*const p_parse_host)(cgpu_ctx *, const uint8_t *const *, const uint16_t *, uint32_t,
@@ -113,7 +114,7 @@ static const any_fn entry_points[] = {
     (any_fn)p_set_ip,         (any_fn)p_last_error,       (any_fn)p_strerror,
     (any_fn)p_parse_frames,   (any_fn)p_nat64_frames,
     (any_fn)p_pkt_status_str, (any_fn)p_abi_version,    (any_fn)p_portmap_reset,
-    (any_fn)p_reconcile,      (any_fn)p_reconcile_frames,
+    (any_fn)p_reconcile,      (any_fn)p_reconcile_frames, (any_fn)p_ctx_check,
 };
 
 int main(void) {
@@ -126,6 +127,7 @@ int main(void) {
   if (p_last_error() != CGPU_EINVAL) return 3;
   if (p_reconcile(NULL, NULL, 0, NULL, NULL, NULL, 0, 0, CGPU_LAYER_L4, NULL, NULL) != CGPU_EINVAL)
     return 5;
+  if (p_ctx_check(NULL, NULL) != CGPU_EINVAL) return 6;
   printf("abi ok: %zu entry points, %s\n", sizeof entry_points / sizeof entry_points[0],
          p_pkt_status_str(CGPU_PKT_NOT_UDP));
   return 0;

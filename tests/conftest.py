@@ -19,3 +19,15 @@ def ctx():
     c = packets.Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture(scope="session")
+def tctx():
+    """A context of the test build (libcapsule_gpu_test.so: capi.hip with
+    CGPU_TEST_HOOKS), for the tests that force rare paths through its
+    environment hooks; the product library reads no environment."""
+    from capsule_amd import packets
+
+    c = packets.Context(0, test_hooks=True)
+    yield c
+    c.close()

@@ -94,3 +94,42 @@ def test_plain_c_consumer_compiles_and_links(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, (r.returncode, r.stderr)
     assert r.stdout.startswith(f"abi ok: {len(N.EXPORTS)} entry points, not a UDP packet.")
+
+
+def test_host_register_takes_whole_pages_only():
+    """cgpu_host_register refuses a base or a size that is not a multiple
+    of the page size (hipHostRegister pins whole pages, so a partial page
+    would pin bytes of other allocations) before it touches the context or
+    the device.  No GPU here: the context argument is a zeroed stand-in that
+    the argument checks never read."""
+    import mmap
+
+    from capsule_amd import synth
+
+    L = N.lib()
+    fake_ctx = ctypes.create_string_buffer(1 << 16)
+    page = mmap.PAGESIZE
+    buf = synth.host_buffer(4 * page)
+    assert buf.nbytes == 4 * page and buf.ctypes.data % page == 0
+    base = buf.ctypes.data
+    for b, n in ((base + 64, 2 * page), (base, 2 * page + 1), (base + page // 2, page),
+                 (base, 100), (base, 0), (0, page)):
+        assert L.cgpu_host_register(fake_ctx, ctypes.c_void_p(b), n) == N.EINVAL, (b - base, n)
+        assert L.cgpu_last_error() == N.EINVAL
+    assert L.cgpu_host_unregister(None, ctypes.c_void_p(base)) == N.EINVAL
+    assert L.cgpu_ctx_check(None, None) == N.EINVAL
+
+
+def test_test_build_is_separate():
+    """The environment hooks live only in the test build: the product
+    library has no getenv reference and none of the hook names."""
+    prod = N.LIB_PATH.read_bytes()
+    for name in (b"CGPU_TEST_SCHED_WAVES", b"CGPU_TEST_SCHED_SPINS", b"CGPU_TEST_NAT64_TAG_MASK"):
+        assert name not in prod, name
+    out = subprocess.run(["nm", "-D", "--undefined-only", str(N.LIB_PATH)], capture_output=True,
+                         text=True, check=True).stdout
+    assert not re.search(r"\bgetenv\b", out)
+    test = N.TEST_LIB_PATH.read_bytes()
+    assert b"CGPU_TEST_SCHED_SPINS" in test
+    T = N.lib(test=True)
+    assert T.cgpu_abi_version() == N.ABI_VERSION

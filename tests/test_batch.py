@@ -268,3 +268,72 @@ def test_group_by_keeps_batch_order_at_scale(ctx):
     assert (out.origin.cpu().numpy() == np.arange(len(o))).all()
     assert (out.batch.off.cpu().numpy().view(np.uint32) == o).all()
     assert seen[6] == int((ok & (proto == 6)).sum())
+
+
+# ---- burst aggregation at the GPU seam (Poll target) --------------------------
+def _rx_bursts(frames, size=32):
+    """An RX queue handing out bursts of at most `size` frames, then empty
+    bursts (rte_eth_rx_burst with nothing left, dpdk/port.rs:149-171)."""
+    chunks = [frames[i:i + size] for i in range(0, len(frames), size)]
+    it = iter(chunks)
+    return lambda: next(it, [])
+
+
+def test_poll_target_gathers_rx_bursts_in_order():
+    frames = [bytes([i & 0xFF, i >> 8]) + bytes(62) for i in range(200)]
+    b = B.Poll(None, _rx_bursts(frames), "cpu", target=100)
+    b.replenish()  # 4 pulls of 32 reach the target
+    out = b.next_burst()
+    assert out.n == 128 and b.pulls == 4
+    assert [out.batch.frame(i) for i in range(out.n)] == frames[:128]
+    b.replenish()  # 32 + 32 + 8, then an empty pull ends the gathering
+    out = b.next_burst()
+    assert out.n == 72 and b.pulls == 4 + 4
+    assert [out.batch.frame(i) for i in range(out.n)] == frames[128:]
+    b.replenish()  # nothing left: no burst, after one pull
+    assert b.next_burst() is None and b.pulls == 9
+    # target=1 is the reference's one pull per replenish
+    one = B.Poll(None, _rx_bursts(frames), "cpu")
+    one.replenish()
+    assert one.next_burst().n == 32 and one.pulls == 1
+
+
+def test_packet_batch_concat_keeps_frames_and_order():
+    rng = np.random.default_rng(3)
+    parts, want = [], []
+    for k in range(3):
+        fr = [bytes(rng.integers(0, 256, int(rng.integers(1, 90)), dtype=np.uint8)) for _ in range(5 + k)]
+        parts.append(B.packets.PacketBatch.from_frames(fr, "cpu", slot=16))
+        want += fr
+    cat = B.packets.PacketBatch.concat(parts)
+    assert cat.n == len(want)
+    assert [cat.frame(i) for i in range(cat.n)] == want
+
+
+@pytest.mark.gpu
+def test_poll_target_parse_matches_oracle(ctx):
+    """IMIX arriving as RX bursts of 32 frames, gathered 2048 at a time and
+    parsed on the device: every packet's parse equals the oracle's on the
+    same frames, in arrival order, the last gather short."""
+    from capsule_amd import synth
+
+    import oracle_lib
+
+    a, o, l = synth.imix(5000, seed=12, vlan_frac=0.1)
+    frames = [bytes(a[int(x):int(x) + int(n)]) for x, n in zip(o, l)]
+    flags = N.F_ACCEPT_ALL | N.F_CSUM_IP | N.F_CSUM_L4 | N.F_FLOW_HASH
+    src = B.Poll(ctx, _rx_bursts(frames), "cuda", target=2048)
+    got_meta, got_hash, sizes = [], [], []
+    while True:
+        src.replenish()
+        pipe = src.parse(flags)
+        out = pipe.next_burst()
+        if out is None:
+            break
+        sizes.append(out.n)
+        got_meta.append(out.parsed.meta.cpu().numpy().view(np.uint32))
+        got_hash.append(out.parsed.flow_hash.cpu().numpy().view(np.uint64))
+    assert sizes == [2048, 2048, 904]
+    om, oc, oh, _ = oracle_lib.parse_batch(a, o, l, flags, fields=False)
+    assert (np.concatenate(got_meta) == om).all()
+    assert (np.concatenate(got_hash) == oh).all()

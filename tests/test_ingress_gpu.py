@@ -7,6 +7,7 @@ staging, and the device reading the registered mempool over PCIe -- and every
 output is compared bit-exactly with the CPU oracle run on the same frames.
 """
 import ctypes
+import mmap
 
 import numpy as np
 import pytest
@@ -49,7 +50,7 @@ def check(ctx, a, o, l, mbufs, ingress, fields=True):
 def test_pageable_mempool_registered_here(ctx, ingress):
     a, o, l = edge_batch()
     mem, mbufs = synth.mbuf_pool(a, o, l)
-    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)  # hipHostRegister
+    reg = packets.HostRegion.of(ctx, mem)  # hipHostRegister
     try:
         check(ctx, a, o, l, mbufs, ingress)
     finally:
@@ -60,9 +61,9 @@ def test_pageable_mempool_registered_here(ctx, ingress):
 def test_pinned_mempool(ctx, ingress):
     a, o, l = synth.imix(4096, seed=3)
     stride = (128 + 128 + int(l.max()) + 63) // 64 * 64
-    pinned = torch.zeros(stride * len(o), dtype=torch.uint8, pin_memory=True)
-    mem, mbufs = synth.mbuf_pool(a, o, l, mem=pinned.numpy())
-    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)  # already page-locked: mapped only
+    pinned, pool = synth.pinned_buffer(stride * len(o))
+    mem, mbufs = synth.mbuf_pool(a, o, l, mem=pool)
+    reg = packets.HostRegion.of(ctx, mem)  # already page-locked: mapped only
     try:
         check(ctx, a, o, l, mbufs, ingress, fields=False)
     finally:
@@ -75,7 +76,7 @@ def test_zero_copy_unaligned_frames(ctx, headroom):
     dword / byte host loads."""
     a, o, l = synth.imix(1500, seed=headroom)
     mem, mbufs = synth.mbuf_pool(a, o, l, headroom=headroom)
-    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    reg = packets.HostRegion.of(ctx, mem)
     try:
         check(ctx, a, o, l, mbufs, N.INGRESS_ZERO_COPY)
     finally:
@@ -88,8 +89,8 @@ def test_zero_copy_two_regions_and_chunking(ctx):
     a2, o2, l2 = synth.uniform(2000, seed=22)
     m1, b1 = synth.mbuf_pool(a1, o1, l1, seed=1)
     m2, b2 = synth.mbuf_pool(a2, o2, l2, seed=2)
-    r1 = packets.HostRegion(ctx, m1.ctypes.data, m1.nbytes)
-    r2 = packets.HostRegion(ctx, m2.ctypes.data, m2.nbytes)
+    r1 = packets.HostRegion.of(ctx, m1)
+    r2 = packets.HostRegion.of(ctx, m2)
     try:
         mb = np.empty(4000, np.uint64)
         mb[0::2], mb[1::2] = b1, b2
@@ -111,7 +112,7 @@ def test_zero_copy_rejects_unregistered_pointers(ctx):
     with pytest.raises(N.CgpuError) as e:
         packets.parse_mbufs(ctx, mbufs, ALL, N.INGRESS_ZERO_COPY)
     assert e.value.code == N.EINVAL
-    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    reg = packets.HostRegion.of(ctx, mem)
     try:
         # an mbuf pointer outside the region
         other = np.zeros(4096, np.uint8)
@@ -150,9 +151,9 @@ def test_register_unregister_bookkeeping(ctx):
     regs = []
     try:
         for b in bufs[:16]:
-            regs.append(packets.HostRegion(ctx, b.ctypes.data, b.nbytes))
+            regs.append(packets.HostRegion.of(ctx, b))
         with pytest.raises(N.CgpuError):  # 16 regions per context
-            packets.HostRegion(ctx, bufs[16].ctypes.data, bufs[16].nbytes)
+            packets.HostRegion.of(ctx, bufs[16])
     finally:
         for r in regs:
             r.close()
@@ -170,7 +171,7 @@ def test_jumbo_mempool(ctx, ingress):
     and the chunk is redone; results bit-exact either way."""
     a, o, l = synth.uniform(700, kind=synth.V4_UDP, frame_len=9000, slot=9024, seed=6)
     mem, mbufs = synth.mbuf_pool(a, o, l, room=9000)
-    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    reg = packets.HostRegion.of(ctx, mem)
     try:
         check(ctx, a, o, l, mbufs, ingress, fields=False)
     finally:
@@ -181,7 +182,7 @@ def test_zero_copy_rejects_frame_past_its_buffer(ctx):
     """data_off + data_len > buf_len is no valid mbuf: the call fails."""
     a, o, l = synth.imix(128, seed=8)
     mem, mbufs = synth.mbuf_pool(a, o, l, room=2048)
-    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    reg = packets.HostRegion.of(ctx, mem)
     try:
         ob = int(mbufs[9]) - mem.ctypes.data
         saved = mem[ob + 40: ob + 42].copy()
@@ -204,7 +205,7 @@ def test_frames_pairs_match_oracle(ctx, ingress):
     mem, mbufs = synth.mbuf_pool(a, o, l)
     addrs, lens = synth.mbuf_frames(mem, mbufs)
     assert (lens == l).all()
-    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    reg = packets.HostRegion.of(ctx, mem)
     try:
         gm, gc, gh, gf = packets.parse_frames(ctx, addrs, lens, ALL, ingress, fields=True)
     finally:
@@ -224,7 +225,7 @@ def test_frames_zero_copy_rejects_unregistered(ctx):
     other = np.zeros(4096, np.uint8)
     addrs = addrs.copy()
     addrs[100] = np.uint64(other.ctypes.data)
-    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    reg = packets.HostRegion.of(ctx, mem)
     try:
         with pytest.raises(N.CgpuError):
             packets.parse_frames(ctx, addrs, lens, ALL, N.INGRESS_ZERO_COPY)
@@ -235,3 +236,73 @@ def test_frames_zero_copy_rejects_unregistered(ctx):
     finally:
         reg.close()
 
+
+
+def test_register_refuses_partial_pages_overlap_and_straddles(ctx):
+    """Whole pages only; no two regions of a context share a page; an
+    already page-locked range is mapped only when one pinned allocation
+    holds all of it."""
+    L = ctx.L
+    page = mmap.PAGESIZE
+    buf = synth.host_buffer(8 * page)
+    base = buf.ctypes.data
+    for b, n in ((base + 64, 4 * page), (base, 4 * page + 64), (base, 100)):
+        assert L.cgpu_host_register(ctx.handle, ctypes.c_void_p(b), n) == N.EINVAL
+    with packets.HostRegion(ctx, base, 4 * page, mem=buf):
+        assert L.cgpu_host_register(ctx.handle, ctypes.c_void_p(base + 2 * page), 4 * page) == N.EINVAL
+        assert L.cgpu_host_register(ctx.handle, ctypes.c_void_p(base), 4 * page) == N.EINVAL
+        with packets.HostRegion(ctx, base + 4 * page, 4 * page):  # the next pages: fine
+            pass
+    t, pool = synth.pinned_buffer(4 * page)
+    pb = pool.ctypes.data
+    with packets.HostRegion.of(ctx, pool):  # one pinned allocation: mapped
+        pass
+    with packets.HostRegion(ctx, pb + page, 2 * page):  # inside it: mapped
+        pass
+    # a range running past the pinned allocation is refused
+    big = 1 << 22
+    assert L.cgpu_host_register(ctx.handle, ctypes.c_void_p(pb), big) == N.EINVAL
+    del t, pool
+
+
+def test_register_unregister_free_then_new_mapping_same_range(ctx):
+    """The fault of round 5: a pinned mapping must not
+    outlive its registration.  A page-aligned pool is registered, read
+    zero-copy, unregistered and unmapped; new memory is mapped over exactly
+    the same range with new bytes; a pageable host-to-device copy of it and a
+    zero-copy read after registering it again must both see the new bytes."""
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                          ctypes.c_int, ctypes.c_long]
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    PROT_RW, MAP_PA, MAP_FIXED_NOREPLACE = 0x3, 0x22, 0x100000
+    a, o, l = synth.imix(2048, seed=61)
+    stride = (128 + 128 + int(l.max()) + 63) // 64 * 64
+    size = (stride * len(o) + mmap.PAGESIZE - 1) // mmap.PAGESIZE * mmap.PAGESIZE
+    p = libc.mmap(None, size, PROT_RW, MAP_PA, -1, 0)
+    assert p not in (None, ctypes.c_void_p(-1).value)
+    mem = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(p))
+    mem, mbufs = synth.mbuf_pool(a, o, l, mem=mem)
+    with packets.HostRegion(ctx, p, size):
+        check(ctx, a, o, l, mbufs, N.INGRESS_ZERO_COPY, fields=False)
+    del mem
+    assert libc.munmap(p, size) == 0
+    q = libc.mmap(p, size, PROT_RW, MAP_PA | MAP_FIXED_NOREPLACE, -1, 0)
+    if q != p:
+        if q not in (None, ctypes.c_void_p(-1).value):
+            libc.munmap(q, size)
+        pytest.skip("the range was taken before it could be mapped again")
+    try:
+        mem2 = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(q))
+        fresh = np.random.default_rng(62).integers(0, 256, size, dtype=np.uint8)
+        mem2[:] = fresh
+        got = torch.from_numpy(mem2).to("cuda:0").cpu().numpy()  # pageable H2D
+        assert (got == fresh).all()
+        a2, o2, l2 = synth.imix(2048, seed=63)
+        mem2, mb2 = synth.mbuf_pool(a2, o2, l2, mem=mem2)
+        with packets.HostRegion(ctx, q, size):
+            check(ctx, a2, o2, l2, mb2, N.INGRESS_ZERO_COPY, fields=False)
+        del mem2
+    finally:
+        libc.munmap(q, size)

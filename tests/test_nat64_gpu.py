@@ -427,17 +427,18 @@ def test_portmap_calls_ordered_across_streams(ctx):
     gw.close()
 
 
-@pytest.mark.parametrize("mask", ["1", "80000000", "0", "zz"])
-def test_claim_tag_collisions_repaired(ctx, monkeypatch, mask):
+@pytest.mark.parametrize("mask", ["0x1", "0x80000000", "0", "zz"])
+def test_claim_tag_collisions_repaired(tctx, monkeypatch, mask):
     """The fused kernel joins a batch-local slot on its 32-bit claim tag; the
     tail compares every joined packet's key with the slot's and repairs a
     collision (distinct keys, equal tags).  With the tags cut to 1 bit
-    (CGPU_TEST_NAT64_TAG_MASK, read when the map is created) half of the
+    (CGPU_TEST_NAT64_TAG_MASK of the test build, read when the map is created) half of the
     meetings of two keys in a probe chain are collisions: ports, frames, map
     state and the 4to6 replies must still equal the oracle's, cold and
-    steady.  A mask of 0 or a value that is not hex is ignored (full tags)."""
+    steady.  A mask of 0 or a value that is not a number is ignored (full tags)."""
     from capsule_amd import packets
 
+    ctx = tctx
     monkeypatch.setenv("CGPU_TEST_NAT64_TAG_MASK", mask)
     gw = packets.Nat64Gateway(ctx, capacity_log2=10)  # 1024 slots, load 0.3
     monkeypatch.delenv("CGPU_TEST_NAT64_TAG_MASK")
@@ -504,7 +505,7 @@ def test_staged_packed_output(ctx, junk):
     gw.close()
 
 
-def test_collision_repair_time_bounded(ctx, monkeypatch):
+def test_collision_repair_time_bounded(tctx, monkeypatch):
     """Round-4 ADVICE: many colliding keys go through the tail's serial
     repair.  With one tag bit kept (about half of 10,000 tag joins collide)
     a 20,000-packet cold batch must still take well under a second, and the
@@ -514,7 +515,8 @@ def test_collision_repair_time_bounded(ctx, monkeypatch):
 
     from capsule_amd import packets
 
-    monkeypatch.setenv("CGPU_TEST_NAT64_TAG_MASK", "1")
+    ctx = tctx
+    monkeypatch.setenv("CGPU_TEST_NAT64_TAG_MASK", "0x1")
     gw = packets.Nat64Gateway(ctx, capacity_log2=14)
     monkeypatch.delenv("CGPU_TEST_NAT64_TAG_MASK")
     pm = oracle_lib.PortMap()

@@ -5,6 +5,8 @@ mbuf.  Checked bit-exactly against the oracle's nat_6to4 / nat_4to6 on the
 same frames: dispositions, statuses, and for every mbuf its data_len, pkt_len
 and frame bytes (Mbuf::shrink / extend keep data_off, mbuf.rs:225-270);
 DROP / ABORT mbufs must be untouched."""
+import mmap
+
 import numpy as np
 import pytest
 
@@ -45,7 +47,7 @@ def _check_mbufs(mem, mbufs, a, o, l, out, out_off, olen, disp):
 
 def _pool(ctx, a, o, l, room):
     mem, mbufs = synth.mbuf_pool(a, o, l, room=room)
-    return mem, mbufs, packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    return mem, mbufs, packets.HostRegion.of(ctx, mem)
 
 
 def test_nat64_mbufs_6to4_then_4to6_replies(ctx):
@@ -263,11 +265,23 @@ def test_nat64_egress_range_checked(ctx):
     out, olen, odisp, _ = pm.nat_6to4(a, o, l)
     keep = np.nonzero(odisp == N.ACT)[0]
     ra, ro, rl = synth.nat64_replies(out, o[keep], olen[keep])
-    mem, mbufs = synth.mbuf_pool(ra, ro, rl, room=2048)
+    # the pool laid out once to find where its last frame ends, then again
+    # `shift` bytes into a page-aligned buffer so that the end + 10 B falls
+    # on a page boundary (regions are whole pages)
+    scratch, mb0 = synth.mbuf_pool(ra, ro, rl, room=2048)
+    a0, l0 = synth.mbuf_frames(scratch, mb0)
+    top = int(np.argmax(a0))
+    end0 = int(a0[top]) + int(l0[top]) + 10 - scratch.ctypes.data
+    page = mmap.PAGESIZE
+    shift = -end0 % page
+    buf = synth.host_buffer(shift + end0 + page)
+    mem, mbufs = synth.mbuf_pool(ra, ro, rl, mem=buf[shift:], room=2048)
     addrs, lens = synth.mbuf_frames(mem, mbufs)
-    top = int(np.argmax(addrs))
-    end = int(addrs[top]) + int(lens[top]) + 10 - mem.ctypes.data
-    reg = packets.HostRegion(ctx, mem.ctypes.data, end)
+    assert int(np.argmax(addrs)) == top
+    end = shift + end0
+    assert end % page == 0
+    reg = packets.HostRegion(ctx, buf.ctypes.data, end)
+    mem = buf
     before = mem.copy()
     try:
         tr = np.full(len(addrs), 100, np.uint16)

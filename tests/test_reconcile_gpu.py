@@ -321,7 +321,7 @@ def test_reconcile_frames_in_registered_mempool(ctx, kind):
         a, o, l = synth.pack_frames(frames)
     mem, mbufs = synth.mbuf_pool(a, o, l)
     addrs, lens = synth.mbuf_frames(mem, mbufs)
-    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    reg = packets.HostRegion.of(ctx, mem)
     try:
         meta = packets.parse_frames(ctx, addrs, lens, ALL, N.INGRESS_ZERO_COPY)[0]
         assert (meta == oracle_lib.parse_batch(a, o, l, ALL)[0]).all()
@@ -346,7 +346,7 @@ def test_reconcile_frames_rejects_unregistered(ctx):
     mem, mbufs = synth.mbuf_pool(a, o, l)
     addrs, lens = synth.mbuf_frames(mem, mbufs)
     other = np.zeros(4096, np.uint8)
-    reg = packets.HostRegion(ctx, mem.ctypes.data, mem.nbytes)
+    reg = packets.HostRegion.of(ctx, mem)
     try:
         meta = packets.parse_frames(ctx, addrs, lens, ALL, N.INGRESS_ZERO_COPY)[0]
         synth.stale_fields(mem, (addrs - np.uint64(mem.ctypes.data)).astype(np.uint32), lens, meta)

@@ -5,15 +5,18 @@ granules.  The order must change no output.
 
 The bench-size batches (1 Mi frames, 16,384 groups against 8,192 resident
 waves) take the schedule in tests/test_bench_parity_gpu.py and
-tests/test_reconcile_gpu.py.  Here the test hook CGPU_TEST_SCHED_WAVES
+tests/test_reconcile_gpu.py.  Here the test build's hook CGPU_TEST_SCHED_WAVES
 (read when a context is created) makes small batches take it: with 256
 resident waves, a batch of 600 groups has its last 256 ordered (whole
 lists of 256 groups, one ordering workgroup each).  Covered:
 IMIX (stream path), 256-B and 1500-B frames (rows path), out-of-order
 descriptors (window path; the scheduler's lightest class), a partial last
 group, reconcile on stale IMIX, more groups than one schedule holds, two
-streams of one context at once (one granule buffer per stream), and graph
-replays (the captured tag; granules cleared by the waves that take them).
+streams of one context at once (one granule buffer per stream), graph
+replays (a captured call runs without the schedule, so replays running at
+once cannot share granules), and a wave that gives up waiting for its group
+(CGPU_TEST_SCHED_SPINS=0): the call must fail loudly, never return stale
+outputs.
 """
 import os
 
@@ -30,13 +33,21 @@ DEV = "cuda:0"
 FLAGS = N.F_ACCEPT_ALL | N.F_FLOW_HASH | N.F_CSUM_IP | N.F_CSUM_L4
 
 
+def _hooked_context(**hooks):
+    """A context of the test build with these CGPU_TEST_* hooks (read when
+    the context is created)."""
+    for k, v in hooks.items():
+        os.environ[k] = str(v)
+    try:
+        return packets.Context(0, test_hooks=True)
+    finally:
+        for k in hooks:
+            del os.environ[k]
+
+
 @pytest.fixture(scope="module")
 def sctx():
-    os.environ["CGPU_TEST_SCHED_WAVES"] = "256"
-    try:
-        c = packets.Context(0)
-    finally:
-        del os.environ["CGPU_TEST_SCHED_WAVES"]
+    c = _hooked_context(CGPU_TEST_SCHED_WAVES=256)
     yield c
     c.close()
 
@@ -134,17 +145,17 @@ def test_two_streams_at_once(sctx):
 
 
 def test_graph_replay_with_new_frames(sctx):
-    """A parse captured into a graph replays with the tag it was captured
-    with; each wave clears the granule it took, so a replay never reads the
-    previous replay's entries.  Three replays over changed frame bytes, each
-    against the oracle."""
+    """A parse captured into a graph runs without the schedule (replays of
+    one graph would share its granule buffer and tag); three replays over
+    changed frame bytes, each against the oracle, then two graphs of the same
+    call replayed on two streams at once."""
     arena, off, ln = synth.imix(64 * 600, seed=31)
     n = len(off)
     b = packets.PacketBatch.from_numpy(arena, off, ln, DEV)
     out = packets.ParseBuffers(n, DEV)
     s = torch.cuda.Stream(DEV)
     with torch.cuda.stream(s):
-        packets.parse(sctx, b, flags=FLAGS, out=out, stream=s)  # the stream's granule buffer
+        packets.parse(sctx, b, flags=FLAGS, out=out, stream=s)
     s.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
@@ -161,3 +172,59 @@ def test_graph_replay_with_new_frames(sctx):
         assert (out.meta.cpu().numpy().view(np.uint32) == om).all()
         assert (out.csum.cpu().numpy().view(np.uint32) == oc).all()
         assert (out.flow_hash.cpu().numpy().view(np.uint64) == oh).all()
+    # two graphs, replayed concurrently on two streams, each its own outputs
+    outs = [packets.ParseBuffers(n, DEV) for _ in range(2)]
+    streams = [torch.cuda.Stream(DEV) for _ in range(2)]
+    graphs = []
+    for o_, st in zip(outs, streams):
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=st):
+            packets.parse(sctx, b, flags=FLAGS, out=o_, stream=st)
+        graphs.append(gr)
+    torch.cuda.synchronize()
+    for _ in range(4):
+        for gr, st in zip(graphs, streams):
+            with torch.cuda.stream(st):
+                gr.replay()
+    torch.cuda.synchronize()
+    sctx.check()
+    om, oc, oh, _ = oracle_lib.parse_batch(b.arena.cpu().numpy(), off, ln, FLAGS, fields=False)
+    for o_ in outs:
+        assert (o_.meta.cpu().numpy().view(np.uint32) == om).all()
+        assert (o_.flow_hash.cpu().numpy().view(np.uint64) == oh).all()
+
+
+def test_give_up_is_reported():
+    """A wave of the ordered range that gives up waiting for its group
+    writes no outputs for it; that must surface as CGPU_EIO: from
+    cgpu_ctx_check after an asynchronous parse, and from the synchronous
+    entry points themselves (here cgpu_parse_host).  CGPU_TEST_SCHED_SPINS=0
+    makes every ordered wave give up at once.  Afterwards the context works
+    (and reports nothing) for a batch that takes no schedule."""
+    c = _hooked_context(CGPU_TEST_SCHED_WAVES=256, CGPU_TEST_SCHED_SPINS=0)
+    try:
+        arena, off, ln = synth.imix(64 * 600, seed=41)
+        b = packets.PacketBatch.from_numpy(arena, off, ln, DEV)
+        out = packets.ParseBuffers(len(off), DEV)
+        out.meta.fill_(-1)
+        packets.parse(c, b, flags=FLAGS, out=out)
+        with pytest.raises(N.CgpuError) as e:
+            c.check()
+        assert e.value.code == N.EIO
+        # the unordered groups were written, the ordered ones (the last 256
+        # groups of 64 frames) were not
+        meta = out.meta.cpu().numpy().view(np.uint32)
+        om = oracle_lib.parse_batch(arena, off, ln, FLAGS, fields=False)[0]
+        assert (meta[:64 * 344] == om[:64 * 344]).all()
+        assert (meta[64 * 344:] == 0xFFFFFFFF).all()
+        c.check()  # read and cleared
+        frames = [bytes(arena[o:o + l]) for o, l in zip(off.tolist(), ln.tolist())]
+        with pytest.raises(N.CgpuError) as e:
+            packets.parse_host(c, frames, flags=FLAGS)
+        assert e.value.code == N.EIO
+        small = frames[:64 * 200]  # one round of waves: no schedule
+        m, _, _, _ = packets.parse_host(c, small, flags=FLAGS)
+        assert (m == om[:len(small)]).all()
+        c.check()
+    finally:
+        c.close()
