@@ -42,6 +42,8 @@ import time
 
 import numpy as np
 
+from capsule_amd.shards import numa_bind
+
 ROOT = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
@@ -608,8 +610,10 @@ def stub_worker(args):
 
     g = ShardGroup()
     same = os.environ.get("CGPU_BENCH_STUB_SAME_DEVICE") == "1"  # (test of check_devices)
-    DEVICES[:] = g.gather_obj({"ordinal": g.local_rank, "name": "stub",
-                               "pci": "stub:00" if same else f"stub:{g.local_rank:02x}"})
+    pci = "0000:00:00" if same else f"0000:{g.local_rank + 1:02x}:00"
+    # no GPU: the binding runs against a sysfs without these devices
+    DEVICES[:] = g.gather_obj({"ordinal": g.local_rank, "name": "stub", "pci": pci,
+                               "numa": numa_bind(pci, sysfs="/nonexistent")})
     check_devices(DEVICES, os.environ.get("CGPU_BENCH_ONE_DEVICE") == "1")
 
     def fake(cfg, steps):
@@ -717,6 +721,9 @@ def main():
     from capsule_amd import packets
     from capsule_amd.shards import ShardGroup
 
+    if args.e2e:  # one rank: its host thread on the GPU's node, then the pinned buffers
+        torch.cuda.set_device(0)
+        numa_bind(device_identity(0)["pci"])
     if args.e2e and args.ingress:
         return e2e_mbufs(args)
     if args.e2e:
@@ -728,7 +735,10 @@ def main():
     ordinal = 0 if one_device else g.local_rank
     dev = torch.device("cuda", ordinal)
     torch.cuda.set_device(dev)
-    DEVICES[:] = g.gather_obj(device_identity(ordinal))
+    ident = device_identity(ordinal)
+    # the rank's host thread on its GPU's NUMA node before any host buffer
+    ident["numa"] = numa_bind(ident["pci"])
+    DEVICES[:] = g.gather_obj(ident)
     check_devices(DEVICES, one_device)
     ctx = packets.Context(ordinal)
 

@@ -739,13 +739,14 @@ static int parse_frames_zero_copy(cgpu_ctx *ctx, const uint8_t *const *pkt, cons
 // kernel reads the frames through the device's mapping of that window, its
 // descriptors (each frame's offset in the window, its length) from
 // page-locked host memory, and writes its results there: one launch and
-// one synchronisation per call, no copy engine and no gather.  This is the
-// latency path for bursts of the RX path's size (RX_BURST_MAX = 32 per
-// rte_eth_rx_burst, port.rs:149-171, aggregated by the caller); past
-// kDirectMax frames the gather path's full-line PCIe reads win
-// (DESIGN.md §8).  Returns 1 when the burst does not qualify (then nothing
-// ran).
-constexpr uint32_t kDirectMax = 1u << 14;
+// one synchronisation per call, no copy engine and no gather: about 20 us
+// per call against the gather path's 73 us, which matters at the RX path's
+// burst sizes (RX_BURST_MAX = 32 per rte_eth_rx_burst, port.rs:149-171,
+// aggregated by the caller), and as fast as the gather up to 2^18 frames
+// (DESIGN.md §8).  Bursts of more than one gather chunk, or spread over
+// several regions, take the gather path.  Returns 1 when the burst does not
+// qualify (then nothing ran).
+constexpr uint32_t kDirectMax = kZcChunk;
 
 static int parse_frames_direct(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *len,
                                uint32_t n, uint32_t flags, uint32_t *meta, uint32_t *csum,
@@ -810,6 +811,40 @@ static int parse_frames_direct(cgpu_ctx *ctx, const uint8_t *const *pkt, const u
   if (fields) memcpy(fields, ctx->h_io + lay.fields, sizeof(cgpu_hdr_record) * (size_t)n);
   if (int e = sync_done(ctx)) return fail(e);
   return ok();
+}
+
+// rte_mbuf bursts on the direct path: the calling core reads each mbuf's
+// data address and length (the header lines it has just written in
+// rte_eth_rx_burst, so in its cache) after checking that the header lies in
+// a registered region and that data_off + data_len <= buf_len, then runs
+// the burst as frame pairs.  Returns 1 when the burst does not qualify
+// (then the device gather runs it, and rejects what is invalid).
+static int parse_mbufs_direct(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32_t flags,
+                              uint32_t *meta, uint32_t *csum, uint64_t *flow_hash,
+                              cgpu_hdr_record *fields) {
+  if (n > kDirectMax) return 1;
+  thread_local std::vector<const uint8_t *> pkt;
+  thread_local std::vector<uint16_t> len;
+  pkt.resize(n);
+  len.resize(n);
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t m = (uint64_t)(uintptr_t)mbufs[i];
+    auto inside = [&](uint32_t q) {
+      return m >= ctx->reg[q].host_base && m + CGPU_MBUF_SIZE <= ctx->reg[q].host_base + ctx->reg[q].bytes;
+    };
+    if (!inside(r)) {
+      for (r = 0; r < ctx->nreg && !inside(r); ++r) {
+      }
+      if (r == ctx->nreg) return 1;
+    }
+    uint16_t blen, doff;
+    memcpy(&blen, (const uint8_t *)mbufs[i] + CGPU_MBUF_BUF_LEN_OFF, 2);
+    memcpy(&doff, (const uint8_t *)mbufs[i] + CGPU_MBUF_DATA_OFF_OFF, 2);
+    mbuf_fields(mbufs[i], pkt[i], len[i]);
+    if ((uint32_t)doff + len[i] > blen) return 1;
+  }
+  return parse_frames_direct(ctx, pkt.data(), len.data(), n, flags, meta, csum, flow_hash, fields);
 }
 
 extern "C" {
@@ -932,8 +967,12 @@ int cgpu_parse_mbufs(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32_t fla
   if (!ctx) return fail(CGPU_EINVAL);
   if (n == 0) return ok();
   if (!mbufs || !meta) return fail(CGPU_EINVAL);
-  if (ingress == CGPU_INGRESS_ZERO_COPY)
+  if (ingress == CGPU_INGRESS_ZERO_COPY) {
+    if (ctx->nreg == 0) return fail(CGPU_EINVAL);
+    const int d = parse_mbufs_direct(ctx, mbufs, n, flags, meta, csum, flow_hash, fields);
+    if (d <= 0) return d;
     return parse_zero_copy(ctx, mbufs, n, flags, meta, csum, flow_hash, fields);
+  }
   if (ingress != CGPU_INGRESS_STAGE) return fail(CGPU_EINVAL);
   auto get = [&](uint32_t i, const uint8_t *&p, uint16_t &l) {
     if (!mbufs[i]) return false;

@@ -165,3 +165,50 @@ def launch_ranks(n, argv, script=None, env=None, timeout=None):
     for p in procs:
         p.wait()
     return rc
+
+
+def _cpulist(text):
+    """'0-3,8,10-11' -> {0, 1, 2, 3, 8, 10, 11} (sysfs cpulist format)."""
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def numa_bind(pci, sysfs="/sys"):
+    """Bind the calling thread (and the threads it starts later) to the CPUs
+    of the NUMA node its GPU hangs off, before the rank allocates any host
+    buffer: one RX queue per core on the GPU's own socket, as capsule's core
+    map pins each core's queues (runtime/core_map.rs:236-293), and page-locked
+    buffers first touched on the node of the GPU's PCIe root.  `pci`:
+    "dddd:bb:dd" (bench.py device_identity).  Returns what was done, for the
+    bench line: {"node", "cpus", "bound", "reason"}."""
+    info = {"node": None, "cpus": 0, "bound": False, "reason": None}
+    try:
+        dom, bus, dev = pci.split(":")
+        path = os.path.join(sysfs, "bus", "pci", "devices", f"{dom}:{bus}:{dev}.0", "numa_node")
+        with open(path) as f:
+            node = int(f.read().strip())
+    except (OSError, ValueError):
+        info["reason"] = "no sysfs numa_node for the GPU"
+        return info
+    info["node"] = node
+    if node < 0:
+        info["reason"] = "the platform reports no NUMA node for the GPU"
+        return info
+    try:
+        with open(os.path.join(sysfs, "devices", "system", "node", f"node{node}", "cpulist")) as f:
+            cpus = _cpulist(f.read())
+    except (OSError, ValueError):
+        info["reason"] = f"no cpulist for node {node}"
+        return info
+    allowed = cpus & os.sched_getaffinity(0)
+    if not allowed:
+        info["reason"] = f"none of node {node}'s CPUs is allowed to this process"
+        return info
+    os.sched_setaffinity(0, allowed)
+    info.update(cpus=len(allowed), bound=True)
+    return info

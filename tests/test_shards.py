@@ -122,7 +122,7 @@ def test_bench_single_gpu_line_shape():
                                "nat64_4to6", "nat64_cold", "reconcile64", "reconcile_imix"}
     for obj in (d["shards"], d["sizes"]["imix"], d["sizes"]["imix_csum"]):
         assert obj["line_floor_bytes"] > 0 and 0 < obj["frac_of_line_floor"]
-    assert d["roofline"]["per_rank"][0]["device"]["pci"] == "stub:00"
+    assert d["roofline"]["per_rank"][0]["device"]["pci"] == "0000:01:00"
     assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(d["roofline"])
     assert "unpinned" in d["parity"]["flow_hash"]
 
@@ -148,6 +148,37 @@ def test_bench_eight_ranks_stub():
     assert [x["rank"] for x in rows] == list(range(8))
     assert len({x["device"]["pci"] for x in rows}) == 8
     assert len(d["shards"]["per_rank"]) == 8
+    # every rank reports its NUMA binding (no GPU here: not bound, and why)
+    for x in rows:
+        numa = x["device"]["numa"]
+        assert set(numa) == {"node", "cpus", "bound", "reason"}
+        assert numa["bound"] is False and numa["reason"]
+
+
+def test_numa_bind_on_a_sysfs_tree(tmp_path):
+    """numa_bind reads the GPU's numa_node and the node's cpulist and pins
+    the calling thread to the node's allowed CPUs (restored afterwards)."""
+    from capsule_amd.shards import _cpulist, numa_bind
+
+    assert _cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    allowed = sorted(os.sched_getaffinity(0))
+    dev = tmp_path / "bus" / "pci" / "devices" / "0000:c1:00.0"
+    dev.mkdir(parents=True)
+    (dev / "numa_node").write_text("1\n")
+    node = tmp_path / "devices" / "system" / "node" / "node1"
+    node.mkdir(parents=True)
+    pick = allowed[: max(1, len(allowed) // 2)]
+    (node / "cpulist").write_text(",".join(map(str, pick)) + ",100000\n")
+    try:
+        info = numa_bind("0000:c1:00", sysfs=str(tmp_path))
+        assert info == {"node": 1, "cpus": len(pick), "bound": True, "reason": None}
+        assert sorted(os.sched_getaffinity(0)) == pick
+    finally:
+        os.sched_setaffinity(0, allowed)
+    (dev / "numa_node").write_text("-1\n")
+    info = numa_bind("0000:c1:00", sysfs=str(tmp_path))
+    assert not info["bound"] and info["node"] == -1
+    assert not numa_bind("0000:c2:00", sysfs=str(tmp_path))["bound"]
 
 
 def test_bench_refuses_shared_device_stub():
