@@ -1011,6 +1011,10 @@ int cgpu_portmap_create(cgpu_ctx *ctx, uint32_t capacity_log2, uint16_t first_po
     std::random_device rd;
     pm->dev.seed_hash = rd();
     pm->dev.seed_tag = rd();
+    for (int j = 0; j < 5; ++j) {  // odd, and not trivially small
+      pm->dev.mul_hash[j] = rd() | 0x80000001u;
+      pm->dev.mul_tag[j] = rd() | 0x80000001u;
+    }
   }
   pm->dev.tag_mask = 0xffffffffu;
 #ifdef CGPU_TEST_HOOKS

@@ -39,7 +39,7 @@ struct ParseArgs {
   uint32_t sched_from = 0, sched_n = 0;
   uint32_t sched_tag = 0;  // this call's granule tag (never 0)
   // A wave that polled its granule sched_spins times without seeing the tag
-  // gives up, takes no group and ORs CGPU_DEVERR_SCHED into *dev_err (the
+  // gives up, takes no group and ORs kDevErrSched into *dev_err (the
   // context's device error word, which cgpu_ctx_check and the synchronous
   // entry points report as CGPU_EIO).
   uint32_t sched_spins = 0;
@@ -99,6 +99,8 @@ struct PortMapDev {
   uint32_t tag_mask;  // claim-tag bits kept (all; a test build of the map keeps fewer:
                       // CGPU_TEST_NAT64_TAG_MASK, to exercise the tail's collision repair)
   uint32_t seed_hash, seed_tag;  // per-map random seeds of key_hash / key_tag
+  // per-map random odd multipliers, one per key word, of key_hash / key_tag
+  uint32_t mul_hash[5], mul_tag[5];
 };
 
 struct Nat64Args {

@@ -77,16 +77,23 @@ __device__ __forceinline__ uint32_t rotl32(uint32_t x, int b) {
   return (x << b) | (x >> (32 - b));
 }
 
-// Both hashes start from a per-map random seed (cgpu_portmap_create), so that
-// keys sharing a probe chain or a claim tag cannot be chosen from outside
-// (crafted collisions would send every such packet through the tail's serial
-// repair): a key word's difference reaches the state through a multiply mod
-// 2^32 of a seed-dependent value, so no difference cancels for every seed.
-__device__ __forceinline__ uint32_t key_hash(const uint32_t (&key)[5], uint32_t seed) {
-  uint32_t h = 0x9e3779b9u ^ seed;
+// Both hashes are keyed per map (cgpu_portmap_create: a random seed and a
+// random odd multiplier per key word for each), so that keys sharing a
+// probe chain or a claim tag cannot be chosen from outside (crafted
+// collisions would send every such packet through the tail's serial
+// repair).  Each key word enters the state multiplied by its own secret
+// multiplier: the state difference two keys leave after word j depends on
+// m_j, so no pair of keys -- and no difference between words j and j + 1 --
+// cancels for every map (with one fixed multiplier, a bit-31 difference in
+// word j and a matching one in word j + 1 cancelled for every seed).  This
+// is a universal-hash argument against keys chosen without knowledge of
+// the map's secrets, not a cryptographic PRF; correctness never depends on
+// it (equal tags are verified on the key words by the tail).
+__device__ __forceinline__ uint32_t key_hash(const uint32_t (&key)[5], const PortMapDev &pm) {
+  uint32_t h = 0x9e3779b9u ^ pm.seed_hash;
 #pragma unroll
   for (int j = 0; j < 5; ++j) {
-    h ^= key[j] * 0xcc9e2d51u;
+    h ^= key[j] * pm.mul_hash[j];
     h = rotl32(h, 13) * 5u + 0xe6546b64u;
   }
   h ^= h >> 16;
@@ -100,11 +107,11 @@ __device__ __forceinline__ uint32_t key_hash(const uint32_t (&key)[5], uint32_t 
 // The claim tag: a second, independent hash of the key (a batch-local slot
 // whose tag differs holds another key; an equal tag is confirmed on the key
 // words).
-__device__ __forceinline__ uint32_t key_tag(const uint32_t (&key)[5], uint32_t seed) {
-  uint32_t h = 0x2545f491u ^ seed;
+__device__ __forceinline__ uint32_t key_tag(const uint32_t (&key)[5], const PortMapDev &pm) {
+  uint32_t h = 0x2545f491u ^ pm.seed_tag;
 #pragma unroll
   for (int j = 0; j < 5; ++j) {
-    h = (h ^ key[j]) * 0x9e3779b1u;
+    h = (h ^ key[j]) * pm.mul_tag[j];
     h ^= h >> 15;
   }
   h *= 0x85ebca77u;
@@ -296,7 +303,7 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
     uint32_t *w = a.pm.slots[h].w;
     uint32_t ref = s0[0], stag = s0[1];
     if (!(ref & kPersist) && !have_tag) {
-      tag = key_tag(key, a.pm.seed_tag) & a.pm.tag_mask;
+      tag = key_tag(key, a.pm) & a.pm.tag_mask;
       have_tag = true;
     }
     if (ref == 0u) {
@@ -337,7 +344,7 @@ __device__ __forceinline__ uint32_t probe_port(const Nat64Args &a, uint32_t i, c
                                                uint32_t &port) {
   uint32_t key[5];
   make_key(v, key);
-  const uint32_t h = key_hash(key, a.pm.seed_hash) & a.pm.cap_mask;
+  const uint32_t h = key_hash(key, a.pm) & a.pm.cap_mask;
   const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
   return probe_port_at(a, i, key, h, sp[0], sp[1], port);
 }
@@ -1033,7 +1040,7 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   const bool act0 = valid && v.disp == CGPU_ACT;
   uint32_t key[5];
   make_key(v, key);
-  const uint32_t h = key_hash(key, a.pm.seed_hash) & a.pm.cap_mask;
+  const uint32_t h = key_hash(key, a.pm) & a.pm.cap_mask;
   u32x4 s0 = {0u, 0u, 0u, 0u}, s1 = {0u, 0u, 0u, 0u};
   if (act0) {
     const u32x4 *sp = reinterpret_cast<const u32x4 *>(&a.pm.slots[h]);
@@ -1348,12 +1355,12 @@ __device__ void tail_repair(const Nat64Args &a, uint32_t nb, uint32_t nmism, con
       add_chunk(a.pm.slots[wrong].w[7]);  // the wrong slot's first packet so far
       const u32x4 sk = a.stash_key[m];
       const uint32_t key[5] = {sk[0], sk[1], sk[2], sk[3], (uint32_t)a.stash_port[m]};
-      uint32_t h = key_hash(key, a.pm.seed_hash) & a.pm.cap_mask, res = kNoSlot;
+      uint32_t h = key_hash(key, a.pm) & a.pm.cap_mask, res = kNoSlot;
       for (uint32_t probe = 0; probe <= a.pm.cap_mask; ++probe, h = (h + 1u) & a.pm.cap_mask) {
         uint32_t *w = a.pm.slots[h].w;
         const uint32_t other[5] = {w[2], w[3], w[4], w[5], w[6] & 0xffffu};
         if (w[0] == 0u) {  // a new key after all: claim it
-          w[1] = key_tag(key, a.pm.seed_tag) & a.pm.tag_mask;
+          w[1] = key_tag(key, a.pm) & a.pm.tag_mask;
           w[2] = key[0];
           w[3] = key[1];
           w[4] = key[2];
