@@ -55,9 +55,19 @@ impl GpuContext {
     }
 
     /// Page-lock and map a mempool's memzone (mempool.rs:64-106) for the
-    /// zero-copy entry points; once per memzone.
+    /// zero-copy entry points; once per memzone.  The memzone is whole pages
+    /// (the library refuses anything else) and stays mapped while the
+    /// context lives: the library borrows it (mbuf.rs:467-479).
     pub fn register_mempool(&mut self, base: *mut u8, len: usize) -> anyhow::Result<()> {
         check(unsafe { g::cgpu_host_register(self.0, base as *mut c_void, len) })
+    }
+
+    /// The context's device error word (cgpu_ctx_check): waits for `stream`
+    /// (null: the default stream) and fails if a kernel of this context
+    /// could not complete its part of a call since the last check.  The
+    /// synchronous calls above check it themselves.
+    pub fn check(&mut self, stream: *mut c_void) -> anyhow::Result<()> {
+        check(unsafe { g::cgpu_ctx_check(self.0, stream) })
     }
 
     /// Parse a burst exactly as `PacketRx::receive` returns it (batch/mod.rs:
