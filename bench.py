@@ -702,6 +702,9 @@ def main():
                          "cgpu_parse_frames (frames, zero-copy)")
     ap.add_argument("--burst", type=int, default=1 << 18,
                     help="with --ingress: mbufs per cgpu_parse_mbufs call")
+    ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
+                    help="with --ingress frames: bursts in flight (2: cgpu_parse_frames_submit "
+                         "/ _wait, the next burst submitted before the previous one is waited for)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -901,19 +904,33 @@ def e2e_mbufs(args):
                                    meta.ctypes.data, cs.ctypes.data, fh.ctypes.data, None),
                 "cgpu_parse_mbufs")
 
+    if args.inflight == 2:
+        if args.ingress != "frames":
+            raise SystemExit("--inflight 2 applies to --ingress frames")
+        pend = []
+
+        def call(k):  # submit burst k, then wait for burst k - 1 (double buffering)
+            a, ln = pairs[k % len(pairs)]
+            pend.append(packets.parse_frames_submit(ctx, a, ln, w["flags"], out=outs[k & 1]))
+            if len(pend) == 2:
+                packets.parse_frames_wait(ctx, pend.pop(0))
+
     for k in range(3):
         call(k)
     calls, t0 = 0, time.perf_counter()
     while calls < max(4, args.steps // 10) or time.perf_counter() - t0 < 2.0:
         call(calls)
         calls += 1
+    if args.inflight == 2:
+        while pend:
+            packets.parse_frames_wait(ctx, pend.pop(0))
     el = time.perf_counter() - t0
     print(json.dumps({
         "metric": "end-to-end Mpps, rte_mbuf bursts from a host mempool ("
                   + ("cgpu_parse_frames: (data_address, data_len) pairs, zero-copy"
                      if args.ingress == "frames" else "cgpu_parse_mbufs") + ")",
         "value": round(calls * B / el / 1e6, 2), "unit": "Mpps", "config": args.config,
-        "ingress": args.ingress, "burst": B, "calls": calls,
+        "ingress": args.ingress, "burst": B, "calls": calls, "inflight": args.inflight,
         "us_per_burst": round(el / calls * 1e6, 1),
         "mempool": f"{n} objects x {stride} B, page-locked, shuffled; 128-B rte_mbuf headers"}),
         flush=True)

@@ -20,7 +20,7 @@ TEST_LIB_PATH = _HERE / "libcapsule_gpu_test.so"
 # ---- constants (include/capsule_gpu.h) ------------------------------------
 ABI_VERSION = 6
 
-OK, EINVAL, ENOMEM, ENODEV, EIO, ENOSPC = 0, -22, -12, -19, -5, -28
+OK, EINVAL, ENOMEM, ENODEV, EIO, ENOSPC, EBUSY = 0, -22, -12, -19, -5, -28, -16
 
 PKT_STATUS = [
     "OK", "ETH_BAD_OFFSET", "ETH_OUT_OF_BUFFER", "NOT_IPV4", "NOT_IPV6", "NOT_IP",
@@ -136,7 +136,7 @@ EXPORTS = [
     "cgpu_pkt_status_str", "cgpu_abi_version", "cgpu_host_register", "cgpu_host_unregister",
     "cgpu_parse_mbufs", "cgpu_set_ip", "cgpu_nat64_mbufs", "cgpu_parse_frames",
     "cgpu_nat64_frames", "cgpu_portmap_reset", "cgpu_reconcile", "cgpu_reconcile_frames",
-    "cgpu_ctx_check",
+    "cgpu_ctx_check", "cgpu_parse_frames_submit", "cgpu_parse_frames_wait",
 ]
 
 _libs = {}
@@ -167,6 +167,10 @@ def lib(test=False):
     L.cgpu_ctx_destroy.argtypes = [vp]
     L.cgpu_ctx_check.restype = i32
     L.cgpu_ctx_check.argtypes = [vp, vp]
+    L.cgpu_parse_frames_submit.restype = i32
+    L.cgpu_parse_frames_submit.argtypes = [vp, vp, vp, u32, u32, vp, vp, vp, P(u32)]
+    L.cgpu_parse_frames_wait.restype = i32
+    L.cgpu_parse_frames_wait.argtypes = [vp, u32]
     L.cgpu_parse_batch.restype = i32
     L.cgpu_parse_batch.argtypes = [vp, P(Batch), u32, P(ParseOut), vp]
     L.cgpu_parse_host.restype = i32

@@ -327,6 +327,42 @@ def parse_frames(ctx, addrs, lens, flags=None, ingress=N.INGRESS_STAGE, fields=F
     return meta, csum, fh, recs
 
 
+class FramesTicket:
+    """A burst in flight through `parse_frames_submit`: its host result
+    arrays (valid once `parse_frames_wait` has returned)."""
+
+    def __init__(self, ticket, meta, csum, flow_hash, keep):
+        self.ticket, self.meta, self.csum, self.flow_hash = ticket, meta, csum, flow_hash
+        self._keep = keep
+
+
+def parse_frames_submit(ctx, addrs, lens, flags=None, out=None):
+    """`cgpu_parse_frames_submit`: start the zero-copy parse of a burst of
+    (data_address, data_len) pairs and return at once (at most two bursts in
+    flight per context; CgpuError EBUSY past that).  `out`: (meta, csum,
+    flow_hash) host arrays to fill, else new ones."""
+    if flags is None:
+        flags = parse_flags()
+    addrs = np.ascontiguousarray(addrs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    n = len(addrs)
+    if out is None:
+        out = (np.zeros(n, np.uint32), np.zeros(n, np.uint32), np.zeros(n, np.uint64))
+    meta, cs, fh = out
+    t = ctypes.c_uint32()
+    N.check(ctx.L.cgpu_parse_frames_submit(ctx.handle, addrs.ctypes.data, lens.ctypes.data, n,
+                                           flags, meta.ctypes.data, cs.ctypes.data,
+                                           fh.ctypes.data, ctypes.byref(t)),
+            "cgpu_parse_frames_submit")
+    return FramesTicket(t.value, meta, cs, fh, out)
+
+
+def parse_frames_wait(ctx, tk):
+    """`cgpu_parse_frames_wait`: the burst's results are in tk's arrays."""
+    N.check(ctx.L.cgpu_parse_frames_wait(ctx.handle, tk.ticket), "cgpu_parse_frames_wait")
+    return tk.meta, tk.csum, tk.flow_hash
+
+
 class Groups:
     """Result of `group_by`: `idx[off[k]:off[k+1]]` are arm k's packets."""
 

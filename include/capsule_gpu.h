@@ -44,7 +44,8 @@ extern "C" {
  *      memory, in place: the mbuf seam of a reconcile combinator).
  *   6  cgpu_ctx_check (the context's device error word); cgpu_host_register
  *      takes whole pages only and refuses ranges it cannot prove are the
- *      caller's; calls captured into a graph run without the wave order.   */
+ *      caller's; calls captured into a graph run without the wave order;
+ *      cgpu_parse_frames_submit / _wait (two bursts in flight).            */
 #define CGPU_ABI_VERSION 6
 
 /* ---- call-level return codes (negative errno style) -------------------- */
@@ -54,6 +55,7 @@ extern "C" {
 #define CGPU_ENODEV (-19)  /* no such HIP device                           */
 #define CGPU_EIO (-5)      /* a HIP runtime call failed                    */
 #define CGPU_ENOSPC (-28)  /* nat64 port table is full                     */
+#define CGPU_EBUSY (-16)   /* cgpu_parse_frames_submit: two bursts in flight */
 
 /* ---- per-packet parse status (low byte of `meta`) -----------------------
  * The first layer of the reference chain Ethernet -> Ipv4|Ipv6 -> Udp|Tcp
@@ -332,6 +334,22 @@ int cgpu_parse_mbufs(cgpu_ctx *ctx, void *const *mbufs, uint32_t n, uint32_t fla
 int cgpu_parse_frames(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *len, uint32_t n,
                       uint32_t flags, uint32_t ingress, uint32_t *meta, uint32_t *csum,
                       uint64_t *flow_hash, cgpu_hdr_record *fields);
+
+/* The same as cgpu_parse_frames with CGPU_INGRESS_ZERO_COPY, split in two
+ * so that the caller's core works on one burst while the device parses the
+ * next (double buffering at the seam of a batch combinator): submit copies
+ * the burst's descriptors, launches, and returns a ticket at once; the
+ * results are in meta / csum / flow_hash (which must stay valid until then;
+ * pkt / len need not) when cgpu_parse_frames_wait(ticket) returns 0.  At
+ * most two bursts per context are in flight: a third submit fails with
+ * CGPU_EBUSY.  Bursts are parsed in submission order.  A burst the one-launch
+ * path cannot take (frames in several registered regions, more than 2^20
+ * frames) is parsed synchronously inside submit, and its wait returns that
+ * call's result.  No header records (use cgpu_parse_frames for those).    */
+int cgpu_parse_frames_submit(cgpu_ctx *ctx, const uint8_t *const *pkt, const uint16_t *len,
+                             uint32_t n, uint32_t flags, uint32_t *meta, uint32_t *csum,
+                             uint64_t *flow_hash, uint32_t *ticket);
+int cgpu_parse_frames_wait(cgpu_ctx *ctx, uint32_t ticket);
 
 /* ---- examples/nat64 6to4 -------------------------------------------------
  * Stateful IPv6 -> IPv4 rewrite of examples/nat64/main.rs:121-150, with the

@@ -37,9 +37,21 @@ pub struct GpuParse<B: Batch<Item = Mbuf>, T: GpuTyped> {
     ctx: GpuContext,
     flags: u32,
     target: usize,
-    out: ParsedBurst,
+    double_buffer: bool,
+    pending: Option<InFlight>,
+    spare: ParsedBurst,
     ready: VecDeque<Disposition<T>>,
     on_parsed: Option<Box<dyn FnMut(&T, &Parsed)>>,
+}
+
+/// A gathered burst on its way through the device: its upstream slots (None
+/// marks an Act packet), the Act mbufs, the results' buffers and the ticket
+/// of its `cgpu_parse_frames_submit` (or the submit's error).
+struct InFlight {
+    slots: Vec<Option<Disposition<Mbuf>>>,
+    act: Vec<Mbuf>,
+    out: ParsedBurst,
+    ticket: anyhow::Result<Option<u32>>,
 }
 
 /// Act packets a GPU combinator gathers from its upstream before one device
@@ -59,7 +71,18 @@ impl<B: Batch<Item = Mbuf>, T: GpuTyped> GpuParse<B, T> {
     /// Explicit flags (T::ACCEPT is always added): e.g. no checksums.
     pub fn with_flags(batch: B, ctx: GpuContext, flags: u32) -> Self {
         GpuParse { batch, ctx, flags: flags | T::ACCEPT, target: GPU_BURST_TARGET,
-                   out: ParsedBurst::default(), ready: VecDeque::new(), on_parsed: None }
+                   double_buffer: true, pending: None, spare: ParsedBurst::default(),
+                   ready: VecDeque::new(), on_parsed: None }
+    }
+
+    /// One burst in flight at a time: each replenish yields the burst it
+    /// gathered (no overlap; the packets leave one poll earlier).  By
+    /// default the device parses the burst just gathered while the packets
+    /// of the previous one are yielded (2x the rate at 512 to
+    /// 4,096 packets).
+    pub fn single_buffered(mut self) -> Self {
+        self.double_buffer = false;
+        self
     }
 
     /// Act packets gathered per device call (1: one call per upstream burst).
@@ -103,16 +126,14 @@ fn drain_bursts<B: Batch>(batch: &mut B, target: usize)
     (slots, act)
 }
 
-impl<B: Batch<Item = Mbuf>, T: GpuTyped> Batch for GpuParse<B, T> {
-    type Item = T;
-
-    fn replenish(&mut self) {
-        let (slots, act) = drain_bursts(&mut self.batch, self.target);
-        // (data_address, data_len) pairs: the device reads the frames alone,
-        // in one launch for bursts of this size (cgpu_parse_frames' direct path)
-        let rc = if act.is_empty() { Ok(()) } else {
-            self.ctx.parse_burst_frames(&act, self.flags, &mut self.out)
-        };
+impl<B: Batch<Item = Mbuf>, T: GpuTyped> GpuParse<B, T> {
+    /// Waits for a burst and yields it in upstream order.
+    fn finish(&mut self, f: InFlight) {
+        let InFlight { slots, act, out, ticket } = f;
+        let rc = ticket.and_then(|t| match t {
+            Some(t) => self.ctx.wait_frames(t),
+            None => Ok(()),
+        });
         let mut act = act.into_iter().enumerate();
         for s in slots {
             let d = match s {
@@ -125,7 +146,7 @@ impl<B: Batch<Item = Mbuf>, T: GpuTyped> Batch for GpuParse<B, T> {
                         // freed when dropped, like any aborted packet
                         Err(e) => Disposition::Abort(anyhow!("GPU parse failed: {}", e)),
                         Ok(()) => {
-                            let parsed = self.out.get(i);
+                            let parsed = out.get(i);
                             match T::from_gpu(mbuf, &parsed) {
                                 Ok(pkt) => {
                                     if let Some(f) = self.on_parsed.as_mut() {
@@ -140,6 +161,36 @@ impl<B: Batch<Item = Mbuf>, T: GpuTyped> Batch for GpuParse<B, T> {
                 }
             };
             self.ready.push_back(d);
+        }
+        self.spare = out;
+    }
+}
+
+impl<B: Batch<Item = Mbuf>, T: GpuTyped> Batch for GpuParse<B, T> {
+    type Item = T;
+
+    fn replenish(&mut self) {
+        let (slots, act) = drain_bursts(&mut self.batch, self.target);
+        let gathered = if slots.is_empty() { None } else {
+            // (data_address, data_len) pairs: the device reads the frames
+            // alone, in one launch (cgpu_parse_frames_submit's direct path)
+            let mut out = std::mem::take(&mut self.spare);
+            let ticket = if act.is_empty() { Ok(None) } else {
+                self.ctx.submit_frames(&act, self.flags, &mut out).map(Some)
+            };
+            Some(InFlight { slots, act, out, ticket })
+        };
+        // the previous burst leaves while this one is parsed; with nothing
+        // new gathered (the queue is drained) the pending burst leaves now
+        if let Some(prev) = self.pending.take() {
+            self.finish(prev);
+        }
+        if let Some(f) = gathered {
+            if self.double_buffer {
+                self.pending = Some(f);
+            } else {
+                self.finish(f);
+            }
         }
     }
 

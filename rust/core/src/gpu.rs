@@ -119,6 +119,32 @@ impl GpuContext {
     }
 }
 
+impl GpuContext {
+    /// `cgpu_parse_frames_submit`: start the parse of a burst's frames and
+    /// return its ticket at once.  The results land in `out`, whose vectors
+    /// must not be touched (moved out, resized or dropped) until
+    /// `wait_frames(ticket)` has returned.  At most two bursts in flight.
+    pub fn submit_frames(&mut self, mbufs: &[Mbuf], flags: u32, out: &mut ParsedBurst)
+                         -> anyhow::Result<u32> {
+        let addrs: Vec<*const u8> =
+            mbufs.iter().map(|m| unsafe { m.data_address(0) } as *const u8).collect();
+        let lens: Vec<u16> = mbufs.iter().map(|m| m.data_len() as u16).collect();
+        out.resize(mbufs.len());
+        let mut ticket = 0u32;
+        check(unsafe {
+            g::cgpu_parse_frames_submit(self.0, addrs.as_ptr(), lens.as_ptr(), mbufs.len() as u32,
+                                        flags, out.meta.as_mut_ptr(), out.csum.as_mut_ptr(),
+                                        out.hash.as_mut_ptr(), &mut ticket)
+        })?;
+        Ok(ticket)
+    }
+
+    /// `cgpu_parse_frames_wait`: the burst of `ticket` is parsed.
+    pub fn wait_frames(&mut self, ticket: u32) -> anyhow::Result<()> {
+        check(unsafe { g::cgpu_parse_frames_wait(self.0, ticket) })
+    }
+}
+
 impl Drop for GpuContext {
     fn drop(&mut self) {
         unsafe { g::cgpu_ctx_destroy(self.0) }

@@ -58,6 +58,10 @@ typedef void (*any_fn)(void);
 static int (*const p_ctx_create)(int, cgpu_ctx **) = cgpu_ctx_create;
 static void (*const p_ctx_destroy)(cgpu_ctx *) = cgpu_ctx_destroy;
 static int (*const p_ctx_check)(cgpu_ctx *, void *) = cgpu_ctx_check;
+static int (*const p_frames_submit)(cgpu_ctx *, const uint8_t *const *, const uint16_t *, uint32_t,
+                                    uint32_t, uint32_t *, uint32_t *, uint64_t *,
+                                    uint32_t *) = cgpu_parse_frames_submit;
+static int (*const p_frames_wait)(cgpu_ctx *, uint32_t) = cgpu_parse_frames_wait;
 static int (*const p_parse_batch)(cgpu_ctx *, const cgpu_batch *, uint32_t,
                                   const cgpu_parse_out *, void *) = cgpu_parse_batch;
 static int (*const p_parse_host)(cgpu_ctx *, const uint8_t *const *, const uint16_t *, uint32_t,
@@ -115,6 +119,7 @@ static const any_fn entry_points[] = {
     (any_fn)p_parse_frames,   (any_fn)p_nat64_frames,
     (any_fn)p_pkt_status_str, (any_fn)p_abi_version,    (any_fn)p_portmap_reset,
     (any_fn)p_reconcile,      (any_fn)p_reconcile_frames, (any_fn)p_ctx_check,
+    (any_fn)p_frames_submit,  (any_fn)p_frames_wait,
 };
 
 int main(void) {
@@ -128,6 +133,7 @@ int main(void) {
   if (p_reconcile(NULL, NULL, 0, NULL, NULL, NULL, 0, 0, CGPU_LAYER_L4, NULL, NULL) != CGPU_EINVAL)
     return 5;
   if (p_ctx_check(NULL, NULL) != CGPU_EINVAL) return 6;
+  if (p_frames_wait(NULL, 1) != CGPU_EINVAL) return 7;
   printf("abi ok: %zu entry points, %s\n", sizeof entry_points / sizeof entry_points[0],
          p_pkt_status_str(CGPU_PKT_NOT_UDP));
   return 0;

@@ -306,3 +306,46 @@ def test_register_unregister_free_then_new_mapping_same_range(ctx):
         del mem2
     finally:
         libc.munmap(q, size)
+
+
+def test_frames_submit_wait_double_buffered(ctx):
+    """cgpu_parse_frames_submit / _wait: bursts submitted two at a time (the
+    next before the previous is waited for), every result against the
+    oracle; a third burst in flight is refused (EBUSY), a stale ticket is
+    EINVAL, and a burst over two regions (no one-launch path) is parsed
+    inside submit and still reported by its wait."""
+    a, o, l = edge_batch(seed=31)
+    mem, mbufs = synth.mbuf_pool(a, o, l)
+    addrs, lens = synth.mbuf_frames(mem, mbufs)
+    om, oc, oh, _ = oracle_lib.parse_batch(a, o, l, ALL, fields=False)
+    cuts = [0, 1, 33, 600, 1700, 2999, 3000]
+    with packets.HostRegion.of(ctx, mem):
+        pend, done = [], []
+        for s, e in zip(cuts[:-1], cuts[1:]):
+            pend.append((s, e, packets.parse_frames_submit(ctx, addrs[s:e], lens[s:e], ALL)))
+            if len(pend) == 2:
+                with pytest.raises(N.CgpuError) as ex:
+                    packets.parse_frames_submit(ctx, addrs[:8], lens[:8], ALL)
+                assert ex.value.code == N.EBUSY
+                s0, e0, tk = pend.pop(0)
+                done.append((s0, e0, packets.parse_frames_wait(ctx, tk)))
+        for s0, e0, tk in pend:
+            done.append((s0, e0, packets.parse_frames_wait(ctx, tk)))
+        for s0, e0, (m, c, h) in done:
+            assert (m == om[s0:e0]).all() and (c == oc[s0:e0]).all() and (h == oh[s0:e0]).all()
+        with pytest.raises(N.CgpuError) as ex:
+            packets.parse_frames_wait(ctx, tk)  # already waited for
+        assert ex.value.code == N.EINVAL
+        # frames in two regions: parsed inside submit, reported by wait
+        a2, o2, l2 = synth.imix(500, seed=32)
+        mem2, mb2 = synth.mbuf_pool(a2, o2, l2)
+        ad2, ln2 = synth.mbuf_frames(mem2, mb2)
+        with packets.HostRegion.of(ctx, mem2):
+            mix_a = np.concatenate([addrs[:300], ad2])
+            mix_l = np.concatenate([lens[:300], ln2])
+            tk = packets.parse_frames_submit(ctx, mix_a, mix_l, ALL)
+            m, c, h = packets.parse_frames_wait(ctx, tk)
+        om2, oc2, oh2, _ = oracle_lib.parse_batch(a2, o2, l2, ALL, fields=False)
+        assert (m == np.concatenate([om[:300], om2])).all()
+        assert (h == np.concatenate([oh[:300], oh2])).all()
+    ctx.check()
