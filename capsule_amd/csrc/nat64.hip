@@ -835,7 +835,10 @@ constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0
 //   17     TCP sum (LE words) of the span bytes among output bytes 0..63
 //   18     v4 pseudo-header sum | VLAN depth << 16
 //   19     output offset
-template <bool K0>
+// FULL: every Act frame of the wave has at least 64 output bytes (no byte
+// mask at the output length within bytes 0..63; the bench's frames, and any
+// TCP frame with 10 B of payload or more).
+template <bool K0, bool FULL>
 __device__ __forceinline__ void rows_build(const uint32_t (&D)[24], const uint32_t (&H)[10],
                                            uint32_t k, uint32_t port_be, uint32_t nl,
                                            uint32_t (&O)[16], uint32_t &acc) {
@@ -846,7 +849,7 @@ __device__ __forceinline__ void rows_build(const uint32_t (&D)[24], const uint32
     const uint32_t x = w < 8 ? D[w] : D[w + 5];  // output bytes >= 32: input + 20
     const uint32_t d = out_dword<true>(r, x, H, port_be);
     uint32_t m = r < 8 ? 0u : (r == 8 ? 0xffff0000u : 0xffffffffu);
-    m &= range_mask(4u * (uint32_t)w, 0u, nl);
+    if (!FULL) m &= range_mask(4u * (uint32_t)w, 0u, nl);
     acc = sad16(d & m, acc);
     O[w] = d;
   }
@@ -939,12 +942,16 @@ __device__ __forceinline__ void rows_store(const Nat64Args &a, rsrc_t ors, const
 // output (out_off[f + 1] = out_off[f] + new length, lengths multiples of 4:
 // the bench's egress image, a TX ring): each half of the wave (16 frames,
 // at most 3,776 B) is assembled in wave-private LDS by the rows and then
-// stored linearly, 1 KiB per instruction.  The 128-B lines that lie wholly
-// inside the half's span are stored nontemporal (whole lines: the output
-// stream then does not push the port map's probe lines out of the L2, as
-// whole-slot nontemporal stores did for 4to6); the half's two boundary lines,
-// which the neighbouring half or wave also writes, keep the default policy.
-constexpr uint32_t kStageDw = 16u * 236u / 4u;  // one half-wave's output, dwords
+// stored linearly, 1 KiB per instruction.  The stage holds the half's bytes
+// at their output address modulo 16 (stage dword 0 is the 16-B chunk the
+// half starts in), so a lane reads each whole output chunk with one aligned
+// 16-B LDS read; only the half's first and last chunks are masked.  The
+// 128-B lines that lie wholly inside the half's span are stored nontemporal
+// (whole lines: the output stream then does not push the port map's probe
+// lines out of the L2, as whole-slot nontemporal stores did for 4to6); the
+// half's two boundary lines, which the neighbouring half or wave also
+// writes, keep the default policy.
+constexpr uint32_t kStageDw = 16u * 236u / 4u + 8u;  // one half-wave's output + alignment, dwords
 constexpr int kStageNT = 2;
 
 __device__ __forceinline__ void rows_store_staged(rsrc_t ors, const u32x4 (&X)[kRowFrames / 4], const uint32_t *lds,
@@ -954,34 +961,30 @@ __device__ __forceinline__ void rows_store_staged(rsrc_t ors, const u32x4 (&X)[k
     const uint32_t S = lds[16u * h * kRowW + 19u];  // the half's first frame's output offset
     const uint32_t *lr = lds + (16u * h + 15u) * kRowW;
     const uint32_t E = lr[19] + lr[16];  // its last frame's end
+    const uint32_t A = S & ~15u;         // the chunk the half starts in: stage dword 0
 #pragma unroll
     for (uint32_t rr = 0; rr < 4u; ++rr) {
       const uint32_t r = 4u * h + rr;
       const uint32_t *fr = lds + (4u * r + row) * kRowW;
       const u32x4 meta = *reinterpret_cast<const u32x4 *>(fr + 16);
       const u32x4 o = rows_chunk(X, fr, r, l, meta);
-      const uint32_t d0 = (meta[3] - S) / 4u + 4u * l;  // the chunk's first dword in the stage
+      const uint32_t d0 = (meta[3] - A) / 4u + 4u * l;  // the chunk's first dword in the stage
 #pragma unroll
       for (uint32_t t = 0; t < 4u; ++t)
         if (16u * l + 4u * t < meta[0]) stage[d0 + t] = o[t];
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const uint32_t A = S & ~15u, nch = (E - A + 15u) >> 4;
+    const uint32_t nch = (E - A + 15u) >> 4;
     for (uint32_t c = lane; c < nch; c += 64u) {
       const uint32_t g = A + 16u * c;
-      u32x4 v;
-#pragma unroll
-      for (uint32_t t = 0; t < 4u; ++t) {
-        const uint32_t b = g + 4u * t;
-        v[t] = b >= S && b < E ? stage[(b - S) / 4u] : 0u;
-      }
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(stage + 4u * c);
       if (g >= S && g + 16u <= E) {
         const uint32_t line = g & ~127u;
         if (line >= S && line + 128u <= E)
           __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)g, 0, kStageNT);
         else
           __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)g, 0, 0);
-      } else {
+      } else {  // the half's first or last chunk: its bytes in [S, E) only
 #pragma unroll
         for (uint32_t t = 0; t < 4u; ++t) {
           const uint32_t b = g + 4u * t;
@@ -1090,8 +1093,10 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
   // and the checksum once the batch order has assigned it).
   const uint32_t k = v.k, port_be = now ? swap16(port & 0xffffu) : 0u;
   uint32_t O[16], accA;
-  if (!__ballot(act && k != 0u)) rows_build<true>(D, H, k, port_be, nl, O, accA);
-  else rows_build<false>(D, H, k, port_be, nl, O, accA);
+  const bool k0 = !__ballot(act && k != 0u), full = !__ballot(act && nl < 64u);
+  if (k0 && full) rows_build<true, true>(D, H, k, port_be, nl, O, accA);
+  else if (k0) rows_build<true, false>(D, H, k, port_be, nl, O, accA);
+  else rows_build<false, false>(D, H, k, port_be, nl, O, accA);
   const uint32_t span = (nl - (34u + 4u * k)) & 0xffffu;
   const uint32_t dst = be32(H[4]);
   const uint32_t ph = fold32(0xcb00u + 0x7101u + (dst >> 16) + (dst & 0xffffu) + 6u + span);
@@ -1117,7 +1122,7 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
 
 __global__ __launch_bounds__(kBlock) NAT64_OCC void nat64_6to4_fused(Nat64Args a) {
   __shared__ uint32_t lds[kBlock / 64][kRowFrames * (kRowW > 24u ? kRowW : 24u)];
-  __shared__ uint32_t stage[kBlock / 64][kStageDw];
+  __shared__ __attribute__((aligned(16))) uint32_t stage[kBlock / 64][kStageDw];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t base = (blockIdx.x * (kBlock / 64u) + wave) * kRowFrames;
   if (base >= a.n) return;  // wave-uniform
