@@ -137,17 +137,20 @@ struct V6 {
 // V6 from frame-relative dwords P[3..16] (bytes 12..67: the VLAN marker
 // through the TCP source port at QinQ depth); the checks follow the
 // reference nat_6to4 control flow in order.
+// NOVLAN: the caller knows that no frame of the wave carries a VLAN marker
+// (static header positions, no per-dword selects).
+template <bool NOVLAN = false>
 __device__ __forceinline__ void classify_dwords(const uint32_t (&P)[20], uint32_t len,
                                                 uint32_t room, V6 &v) {
   const uint32_t marker = be16_lo(P[3]);
-  v.k = marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u);
+  v.k = NOVLAN ? 0u : (marker == 0x8100u ? 1u : (marker == 0x88a8u ? 2u : 0u));
   v.eth_len = 14u + 4u * v.k;
-  const uint32_t et = be16_lo(sel3(v.k, P[3], P[4], P[5]));
+  const uint32_t et = NOVLAN ? marker : be16_lo(sel3(v.k, P[3], P[4], P[5]));
   uint32_t A[13];
 #pragma unroll
-  for (int j = 0; j < 13; ++j) A[j] = __builtin_amdgcn_alignbyte(P[4 + j], P[3 + j], 2);
+  for (int j = 0; j < (NOVLAN ? 11 : 13); ++j) A[j] = __builtin_amdgcn_alignbyte(P[4 + j], P[3 + j], 2);
 #pragma unroll
-  for (int j = 0; j < 11; ++j) v.L[j] = sel3(v.k, A[j], A[j + 1], A[j + 2]);
+  for (int j = 0; j < 11; ++j) v.L[j] = NOVLAN ? A[j] : sel3(v.k, A[j], A[j + 1], A[j + 2]);
   v.disp = CGPU_ABORT;
   // packet.parse::<Ethernet>()? (ethernet.rs:279-300)
   if (len == 0u) { v.st = CGPU_PKT_ETH_BAD_OFFSET; return; }
@@ -833,7 +836,9 @@ constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0
 //   0..15  output bytes 0..63 (TCP checksum field zero)
 //   16     output length if the frame is finished here, else 0
 //   17     TCP sum (LE words) of the span bytes among output bytes 0..63
-//   18     v4 pseudo-header sum | VLAN depth << 16
+//          (after A5: the whole span's sum)
+//   18     v4 pseudo-header sum | VLAN depth << 16 (after A5: the finished
+//          TCP checksum field | VLAN depth << 16)
 //   19     output offset
 // FULL: every Act frame of the wave has at least 64 output bytes (no byte
 // mask at the output length within bytes 0..63; the bench's frames, and any
@@ -911,9 +916,8 @@ __device__ __forceinline__ u32x4 rows_chunk(const u32x4 (&X)[kRowFrames / 4], co
                                             uint32_t l, const u32x4 &meta) {
   const u32x4 hc = *reinterpret_cast<const u32x4 *>(fr + 4u * (l & 3u));
   u32x4 o = l < 4u ? hc : X[r];
-  if (l == 3u) {
-    const uint32_t fk = meta[2] >> 16, fph = meta[2] & 0xffffu;
-    const uint32_t tcp_c = (~fold32(fph + swap16(fold32(meta[1])))) & 0xffffu;
+  if (l == 3u) {  // the checksum, finished by the frame's own lane in A5
+    const uint32_t fk = meta[2] >> 16, tcp_c = meta[2] & 0xffffu;
 #pragma unroll
     for (uint32_t t = 0; t < 4u; ++t)
       if (t == fk) o[t] |= swap16(tcp_c) << 16;
@@ -1039,7 +1043,9 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
 #pragma unroll
   for (int j = 0; j < 20; ++j) P[j] = D[j];
   V6 v;
-  classify_dwords(P, len, a.room, v);
+  const uint32_t mk = be16_lo(P[3]);
+  if (!__ballot(mine && (mk == 0x8100u || mk == 0x88a8u))) classify_dwords<true>(P, len, a.room, v);
+  else classify_dwords<false>(P, len, a.room, v);
   const bool act0 = valid && v.disp == CGPU_ACT;
   uint32_t key[5];
   make_key(v, key);
@@ -1105,10 +1111,11 @@ __device__ __forceinline__ bool rows_6to4(const Nat64Args &a, rsrc_t rs, rsrc_t 
     for (int m = 0; m < 4; ++m)
       *reinterpret_cast<u32x4 *>(rec + 4 * m) = u32x4{O[4 * m], O[4 * m + 1], O[4 * m + 2], O[4 * m + 3]};
     const uint32_t payload = rec[17];
-    *reinterpret_cast<u32x4 *>(rec + 16) =
-        u32x4{act ? nl : 0u, payload + accA, ph | (k << 16), o_off};
-    // a deferred frame's checksum (with port 0) and VLAN depth, for the tail
-    if (deferred) a.stash_c0[i] = ((~fold32(ph + swap16(fold32(payload + accA)))) & 0xffffu) | (k << 16);
+    // the TCP checksum field (a deferred frame's with port 0, stashed with
+    // its VLAN depth for the tail), once per frame rather than per row store
+    const uint32_t c0k = ((~fold32(ph + swap16(fold32(payload + accA)))) & 0xffffu) | (k << 16);
+    *reinterpret_cast<u32x4 *>(rec + 16) = u32x4{act ? nl : 0u, payload + accA, c0k, o_off};
+    if (deferred) a.stash_c0[i] = c0k;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   // the staged store: every frame of the wave Act, the outputs tiling one
@@ -1789,9 +1796,8 @@ __device__ __forceinline__ void rows_store6(const Nat64Args &a, rsrc_t ors, cons
     if (!__ballot(fnl != 0u)) continue;
     const u32x4 hc = *reinterpret_cast<const u32x4 *>(fr + 4u * (l < 5u ? l : 0u));
     u32x4 o = l < 5u ? hc : X[r];
-    if (l == 4u) {
-      const uint32_t fk = meta[2] >> 16, fph = meta[2] & 0xffffu;
-      const uint32_t tcp_c = (~fold32(fph + swap16(fold32(meta[1])))) & 0xffffu;
+    if (l == 4u) {  // the checksum, finished by the frame's own lane in A5
+      const uint32_t fk = meta[2] >> 16, tcp_c = meta[2] & 0xffffu;
 #pragma unroll
       for (uint32_t t = 0; t < 4u; ++t)
         if (t == fk + 1u) o[t] |= swap16(tcp_c) << 16;
@@ -1883,7 +1889,8 @@ __device__ __forceinline__ bool rows_4to6(const Nat64Args &a, rsrc_t rs, rsrc_t 
     for (int m = 0; m < 5; ++m)
       *reinterpret_cast<u32x4 *>(rec + 4 * m) = u32x4{O[4 * m], O[4 * m + 1], O[4 * m + 2], O[4 * m + 3]};
     const uint32_t payload = rec[21];
-    *reinterpret_cast<u32x4 *>(rec + 20) = u32x4{act ? nl : 0u, payload + accA, fph | (k << 16), o_off};
+    const uint32_t tcp_c = (~fold32(fph + swap16(fold32(payload + accA)))) & 0xffffu;
+    *reinterpret_cast<u32x4 *>(rec + 20) = u32x4{act ? nl : 0u, payload + accA, tcp_c | (k << 16), o_off};
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   rows_store6(a, ors, X, lds, row, l);
