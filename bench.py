@@ -830,10 +830,31 @@ def bench_nat64_mbufs(args, w):
             return d
         return gw.nat_mbufs(bursts[k % len(bursts)], direction)[0]
 
+    # Each call rewrites its burst's objects in place; they are restored
+    # between calls, outside the timed region: for bursts of up to 8 Ki
+    # mbufs only the burst's own objects (header line + frame), so the
+    # restore does not sweep the whole pool through the CPU caches before
+    # each call (whose host-side work it would then slow down)
+    mb_off = (mbufs.astype(np.int64) - mem.ctypes.data)
+    nobj = 128 + 128 + int(w["len"].max()) + 20
+    restore = None
+    if B <= 8192 and n * nobj <= 1 << 26:
+        rel = np.arange(nobj, dtype=np.int64)
+        restore = [(mb_off[s:s + B, None] + rel[None, :]).ravel().astype(np.int32)
+                   for s in range(0, n - B + 1, B)]
+
+    def reset(k):
+        if restore is None:
+            np.copyto(mem, orig)
+        else:
+            idx = restore[k % len(restore)]
+            mem[idx] = orig[idx]
+
     call(0)  # 6to4: first sight of the keys (deferred path), untimed
+    reset(0)
     calls, el, acts = 0, 0.0, 0
     while calls < max(4, args.steps // 50) or el < 1.0:
-        np.copyto(mem, orig)
+        reset(calls)
         t0 = time.perf_counter()
         disp = call(calls)
         el += time.perf_counter() - t0

@@ -1405,6 +1405,125 @@ static int nat64_mbufs(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm, void *const *m
   return ok();
 }
 
+// nat64 over frame pairs, direct: when every frame (with the 20 bytes a
+// 4to6 rewrite may grow into, where its tailroom allows it) lies in one
+// registered region, the fused kernel reads the frames through the device's
+// mapping of that region, its descriptors from page-locked host memory, and
+// writes the dispositions, statuses and new lengths there; the scatter
+// writes every ACT frame back into its own buffer.  One synchronisation per
+// call, no gather and no copies.  6to4 rewrites each frame in
+// place (its output, 20 B shorter, starts where it does: every output byte
+// j comes from input byte j + 20 or later, which the kernel has loaded
+// before it stores j); 4to6 output passes through a device arena (frame i
+// at i * kNatSlot) and the scatter, since a frame longer than one 256-B
+// pass would read bytes its own first pass had already grown over.
+// Returns 1 when the burst does not qualify (then nothing ran).
+constexpr uint32_t kNatSlot = 2112;  // >= 2048 + 20, a multiple of 64
+
+static int nat64_frames_direct(bool to4, cgpu_ctx *ctx, cgpu_portmap *pm,
+                               const uint8_t *const *frames, const uint16_t *flen,
+                               const uint16_t *ftail, uint32_t n, uint16_t *out_len,
+                               uint8_t *disposition, uint8_t *status) {
+  if (n > kDirectMax) return 1;
+  uint32_t r = 0;
+  const uint64_t a0 = (uint64_t)(uintptr_t)frames[0];
+  for (; r < ctx->nreg; ++r)
+    if (a0 >= ctx->reg[r].host_base && a0 + flen[0] <= ctx->reg[r].host_base + ctx->reg[r].bytes) break;
+  if (r == ctx->nreg) return 1;
+  const uint64_t rb = ctx->reg[r].host_base, re = rb + ctx->reg[r].bytes;
+  uint64_t lo = a0, hi = a0 + flen[0];
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t a = (uint64_t)(uintptr_t)frames[i];
+    if (flen[i] > 2048u) return 1;
+    // the bytes the call may write: 4to6 grows a frame with the room by 20
+    const uint64_t e = a + flen[i] + (!to4 && ftail[i] > 20u ? 20u : 0u);
+    if (a < rb || e > re) return 1;
+    lo = a < lo ? a : lo;
+    hi = e > hi ? e : hi;
+  }
+  lo &= ~(uint64_t)255u;
+  if (lo < rb) lo = rb;
+  if (hi - lo > 0xffff0000ull) return 1;
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok()) return fail(CGPU_ENODEV);
+  if (int e = grow_dev(&ctx->d_out, &ctx->out_cap, (size_t)n * kNatSlot + 64)) return fail(e);
+  // page-locked: off | len | out_off | out_len | disp | status | fr_dev | tailroom
+  const size_t o_off = 0, o_len = align_up(4ull * n, 256), o_oo = o_len + align_up(2ull * n, 256);
+  const size_t o_ol = o_oo + align_up(4ull * n, 256), o_d = o_ol + align_up(2ull * n, 256);
+  const size_t o_st = o_d + align_up(n, 256), o_fr = o_st + align_up(n, 256);
+  const size_t o_tr = o_fr + align_up(8ull * n, 256), o_end = o_tr + align_up(4ull * n, 256);
+  cgpu_ctx::IoSlot &slot = ctx->io[2];
+  if (o_end > slot.cap) {
+    if (slot.h) (void)hipHostFree(slot.h);
+    slot.h = slot.d = nullptr;
+    slot.cap = 0;
+    const size_t cap = align_up(o_end + o_end / 2, 1u << 16);
+    if (hipHostMalloc((void **)&slot.h, cap, hipHostMallocDefault) != hipSuccess) return fail(CGPU_ENOMEM);
+    if (hipHostGetDevicePointer((void **)&slot.d, slot.h, 0) != hipSuccess || !slot.d) {
+      (void)hipHostFree(slot.h);
+      slot.h = nullptr;
+      return fail(CGPU_EIO);
+    }
+    slot.cap = cap;
+  }
+  uint8_t *H = slot.h, *D = slot.d;
+  uint32_t *hoff = (uint32_t *)(H + o_off), *hoo = (uint32_t *)(H + o_oo), *htr = (uint32_t *)(H + o_tr);
+  uint64_t *hfr = (uint64_t *)(H + o_fr);
+  const uint64_t db = ctx->reg[r].dev_base - rb;  // host address -> device address
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t a = (uint64_t)(uintptr_t)frames[i];
+    hoff[i] = (uint32_t)(a - lo);
+    hoo[i] = i * kNatSlot;
+    hfr[i] = flen[i] ? a + db : 0ull;  // an empty frame is never ACT
+    htr[i] = ftail ? ftail[i] : 0u;
+  }
+  memcpy(H + o_len, flen, 2ull * n);
+  cgpu_batch in;
+  in.arena = (const uint8_t *)(uintptr_t)(ctx->reg[r].dev_base + (lo - rb));
+  in.arena_len = hi - lo;
+  in.off = (const uint32_t *)(D + o_off);
+  in.len = (const uint16_t *)(D + o_len);
+  in.n = n;
+  pm->room = 65535u;  // the scatter applies each frame's real tailroom
+  // 6to4: in place, out_off = off over the same window
+  uint8_t *oa = to4 ? (uint8_t *)(uintptr_t)in.arena : ctx->d_out;
+  const uint64_t oa_len = to4 ? in.arena_len : (uint64_t)n * kNatSlot + 64;
+  const uint32_t *oo = to4 ? in.off : (const uint32_t *)(D + o_oo);
+  const int e = nat64_call(to4, ctx, pm, &in, oa, oa_len, oo, (uint16_t *)(D + o_ol), D + o_d, D + o_st,
+                           ctx->stream);
+  pm->room = 2048u;
+  if (e) return e;
+  if (to4) {
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(CGPU_EIO);
+    memcpy(disposition, H + o_d, n);
+    memcpy(status, H + o_st, n);
+    const uint16_t *ol = (const uint16_t *)(H + o_ol);
+    for (uint32_t i = 0; i < n; ++i) out_len[i] = disposition[i] == CGPU_ACT ? ol[i] : 0;
+    return ok();
+  }
+  cgpu::ScatterArgs sc;
+  sc.out_arena = ctx->d_out;
+  sc.out_off = (const uint32_t *)(D + o_oo);
+  sc.out_len = (const uint16_t *)(D + o_ol);
+  sc.disposition = D + o_d;
+  sc.status = D + o_st;
+  sc.mb_dev = nullptr;
+  sc.fr_dev = (const uint64_t *)(D + o_fr);
+  sc.pkt_len = nullptr;
+  sc.tailroom = (const uint32_t *)(D + o_tr);
+  sc.in_len = in.len;
+  sc.n = n;
+  sc.delta = to4 ? -20 : 20;
+  if (cgpu::launch_mbuf_scatter(sc, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess)
+    return fail(CGPU_EIO);
+  memcpy(disposition, H + o_d, n);
+  memcpy(status, H + o_st, n);
+  const uint16_t *ol = (const uint16_t *)(H + o_ol);
+  for (uint32_t i = 0; i < n; ++i) out_len[i] = disposition[i] == CGPU_ACT ? ol[i] : 0;
+  return ok();
+}
+
 int cgpu_nat64_mbufs(cgpu_ctx *ctx, cgpu_portmap *pm, uint32_t direction, void *const *mbufs,
                      uint32_t n, uint8_t *disposition, uint8_t *status) {
   if (direction != CGPU_NAT64_6TO4 && direction != CGPU_NAT64_4TO6) return fail(CGPU_EINVAL);
@@ -1416,8 +1535,13 @@ int cgpu_nat64_frames(cgpu_ctx *ctx, cgpu_portmap *pm, uint32_t direction,
                       uint32_t n, uint16_t *out_len, uint8_t *disposition, uint8_t *status) {
   if (direction != CGPU_NAT64_6TO4 && direction != CGPU_NAT64_4TO6) return fail(CGPU_EINVAL);
   if (n != 0 && !frames) return fail(CGPU_EINVAL);
-  return nat64_mbufs(direction == CGPU_NAT64_6TO4, ctx, pm, nullptr, n, disposition, status, frames,
-                     len, tailroom, out_len);
+  const bool to4 = direction == CGPU_NAT64_6TO4;
+  if (ctx && pm && n != 0 && len && out_len && disposition && status && ctx->nreg != 0 &&
+      (to4 || tailroom)) {
+    const int d = nat64_frames_direct(to4, ctx, pm, frames, len, tailroom, n, out_len, disposition, status);
+    if (d <= 0) return d;
+  }
+  return nat64_mbufs(to4, ctx, pm, nullptr, n, disposition, status, frames, len, tailroom, out_len);
 }
 
 int cgpu_group_by(cgpu_ctx *ctx, const void *key, uint32_t key_kind, uint32_t n,
@@ -1560,51 +1684,65 @@ int cgpu_reconcile_frames(cgpu_ctx *ctx, uint8_t *const *frames, const uint16_t 
   }
   DeviceGuard dg(ctx->device);
   if (!dg.ok()) return fail(CGPU_ENODEV);
-  // staging: off u32 | len u16 | meta u32 | status u8, per region's frames
+  // off u32 | len u16 | meta u32 | status u8 in page-locked host memory the
+  // kernels read and write through its device mapping (no copies), each
+  // region's frames in their own range; one synchronisation for the call
   const size_t o_off = 0, o_len = align_up(4ull * n, 256), o_meta = o_len + align_up(2ull * n, 256);
   const size_t o_st = o_meta + align_up(4ull * n, 256), o_end = o_st + align_up(n, 256);
-  if (int e = grow(&ctx->h_desc, &ctx->d_desc, &ctx->desc_cap, o_end)) return fail(e);
-  uint8_t *D = ctx->d_desc, *H = ctx->h_desc;
+  cgpu_ctx::IoSlot &slot = ctx->io[2];
+  if (o_end > slot.cap) {
+    if (slot.h) (void)hipHostFree(slot.h);
+    slot.h = slot.d = nullptr;
+    slot.cap = 0;
+    const size_t cap = align_up(o_end + o_end / 2, 1u << 16);
+    if (hipHostMalloc((void **)&slot.h, cap, hipHostMallocDefault) != hipSuccess) return fail(CGPU_ENOMEM);
+    if (hipHostGetDevicePointer((void **)&slot.d, slot.h, 0) != hipSuccess || !slot.d) {
+      (void)hipHostFree(slot.h);
+      slot.h = nullptr;
+      return fail(CGPU_EIO);
+    }
+    slot.cap = cap;
+  }
+  uint8_t *D = slot.d, *H = slot.h;
   hipStream_t s = ctx->stream;
   if ((flags & (CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6)) == 0) flags |= CGPU_F_ACCEPT_V4 | CGPU_F_ACCEPT_V6;
   if ((flags & (CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP | CGPU_F_ACCEPT_ICMP)) == 0)
     flags |= CGPU_F_ACCEPT_UDP | CGPU_F_ACCEPT_TCP;
+  uint32_t first[cgpu::kMaxRegions], fill[cgpu::kMaxRegions];
+  for (uint32_t r = 0, acc = 0; r < ctx->nreg; ++r) {
+    first[r] = fill[r] = acc;
+    acc += cnt[r];
+  }
+  uint32_t *ho = (uint32_t *)(H + o_off), *hm = (uint32_t *)(H + o_meta);
+  uint16_t *hl = (uint16_t *)(H + o_len);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t r = region[i], q = fill[r]++;
+    ho[q] = (uint32_t)((uint64_t)(uintptr_t)frames[i] - lo[r]);
+    hl[q] = len[i];
+    hm[q] = meta[i];
+  }
   for (uint32_t r = 0; r < ctx->nreg; ++r) {
     if (!cnt[r]) continue;
-    uint32_t *ho = (uint32_t *)(H + o_off), *hm = (uint32_t *)(H + o_meta);
-    uint16_t *hl = (uint16_t *)(H + o_len);
-    uint32_t m = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-      if (region[i] != r) continue;
-      ho[m] = (uint32_t)((uint64_t)(uintptr_t)frames[i] - lo[r]);
-      hl[m] = len[i];
-      hm[m] = meta[i];
-      ++m;
-    }
-    if (hipMemcpyAsync(D, H, o_st, hipMemcpyHostToDevice, s) != hipSuccess) return fail(CGPU_EIO);
     uint8_t *win = (uint8_t *)(uintptr_t)(ctx->reg[r].dev_base + (lo[r] - ctx->reg[r].host_base));
     cgpu::ParseArgs a{};
     a.arena = win;
     a.arena_len = (uint32_t)(hi[r] - lo[r]);
-    a.off = (const uint32_t *)(D + o_off);
-    a.len = (const uint16_t *)(D + o_len);
-    a.n = m;
+    a.off = (const uint32_t *)(D + o_off) + first[r];
+    a.len = (const uint16_t *)(D + o_len) + first[r];
+    a.n = cnt[r];
     a.accept = flags & (CGPU_F_ACCEPT_ALL | CGPU_F_ACCEPT_ICMP | CGPU_F_V6_EXT);
     a.wr_arena = win;
-    a.meta_in = (const uint32_t *)(D + o_meta);
+    a.meta_in = (const uint32_t *)(D + o_meta) + first[r];
     a.depth = depth;
-    a.rstatus = D + o_st;
+    a.rstatus = D + o_st + first[r];
     set_schedule(ctx, a, s);
     hipError_t e = cgpu::launch_reconcile(a, s);
     if (e != hipSuccess) return hip_fail(e);
-    if (hipMemcpyAsync(H + o_st, D + o_st, m, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-      return fail(CGPU_EIO);
-    if (status) {
-      uint32_t q = 0;
-      for (uint32_t i = 0; i < n; ++i)
-        if (region[i] == r) status[i] = H[o_st + q++];
-    }
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) return fail(CGPU_EIO);
+  if (status) {
+    for (uint32_t r = 0; r < ctx->nreg; ++r) fill[r] = first[r];
+    for (uint32_t i = 0; i < n; ++i) status[i] = H[o_st + fill[region[i]]++];
   }
   if (int e = sync_done(ctx)) return fail(e);
   return ok();

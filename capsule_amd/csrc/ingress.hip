@@ -200,46 +200,38 @@ __global__ __launch_bounds__(kBlock) void mbuf_gather(GatherArgs g) {
 // mbuf.rs:225-270), and data_len / pkt_len adjusted by the same delta.  4to6
 // first applies extend's tailroom check (`20 < tailroom`, mbuf.rs:228) with
 // the mbuf's real buf_len: a frame without the room is ABORT / NOT_RESIZED
-// and its mbuf is left as it was.  16-lane groups write four frames per
-// round, 16 B per lane, as posted PCIe writes to the registered mempool.
+// and its mbuf is left as it was.  A 16-lane group per frame, 16 B per lane
+// and 256 B per group and instruction, as posted PCIe writes to the
+// registered mempool: every frame's bytes are in flight after one read of
+// its metadata and one of its output, so a burst of a few thousand frames
+// costs a couple of round trips, not one per frame of a wave.
 __global__ __launch_bounds__(kBlock) void mbuf_scatter(ScatterArgs a) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t lane = threadIdx.x & 63u;
-  bool act = false;
-  uint32_t nl = 0;
-  if (i < a.n && a.disposition[i] == CGPU_ACT && a.fr_dev[i] != 0ull) {
-    act = true;
-    if (a.delta > 0 && !((uint32_t)a.delta < a.tailroom[i])) {
-      act = false;
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i = t >> 4, gl = t & 15u;
+  if (i >= a.n) return;
+  if (a.disposition[i] != CGPU_ACT || a.fr_dev[i] == 0ull) return;
+  if (a.delta > 0 && !((uint32_t)a.delta < a.tailroom[i])) {
+    if (gl == 0u) {
       a.disposition[i] = CGPU_ABORT;
       a.status[i] = CGPU_PKT_NOT_RESIZED;
-    } else {
-      nl = a.out_len[i];
-      if (a.mb_dev[i] != 0ull) {  // frame pairs: the caller updates the mbuf
-        uint8_t *h = reinterpret_cast<uint8_t *>(a.mb_dev[i]);
-        *reinterpret_cast<uint16_t *>(h + CGPU_MBUF_DATA_LEN_OFF) = (uint16_t)nl;
-        *reinterpret_cast<uint32_t *>(h + CGPU_MBUF_PKT_LEN_OFF) = a.pkt_len[i] + (uint32_t)a.delta;
-      }
     }
+    return;
   }
-  const uint32_t o = act ? a.out_off[i] : 0u;
-  const uint64_t dst = act ? a.fr_dev[i] : 0ull;
-  const uint32_t grp = lane >> 4, gl = lane & 15u;
-  for (uint32_t r = 0; r < 16u; ++r) {
-    const uint32_t f = 4u * r + grp;
-    const uint32_t fl = __shfl(nl, (int)f);
-    if (!__ballot(fl != 0u)) continue;
-    const uint64_t fd = __shfl(dst, (int)f);
-    const uint32_t fo = __shfl(o, (int)f);
-    for (uint32_t pos = 16u * gl; pos < fl; pos += 256u) {
-      const u32x4 v = *reinterpret_cast<const u32x4 *>(a.out_arena + fo + pos);
-      uint8_t *p = reinterpret_cast<uint8_t *>(fd + pos);
-      const uint32_t r16 = fl - pos;
-      if (((fd + pos) & 15u) == 0u && r16 >= 16u) {
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
-      } else {
-        for (uint32_t b = 0; b < 16u && b < r16; ++b) p[b] = (uint8_t)(v[b >> 2] >> (8u * (b & 3u)));
-      }
+  const uint32_t nl = a.out_len[i], fo = a.out_off[i];
+  const uint64_t fd = a.fr_dev[i];
+  if (gl == 0u && a.mb_dev != nullptr && a.mb_dev[i] != 0ull) {  // rte_mbufs (not frame pairs)
+    uint8_t *h = reinterpret_cast<uint8_t *>(a.mb_dev[i]);
+    *reinterpret_cast<uint16_t *>(h + CGPU_MBUF_DATA_LEN_OFF) = (uint16_t)nl;
+    *reinterpret_cast<uint32_t *>(h + CGPU_MBUF_PKT_LEN_OFF) = a.pkt_len[i] + (uint32_t)a.delta;
+  }
+  for (uint32_t pos = 16u * gl; pos < nl; pos += 256u) {
+    const u32x4 v = *reinterpret_cast<const u32x4 *>(a.out_arena + fo + pos);
+    uint8_t *p = reinterpret_cast<uint8_t *>(fd + pos);
+    const uint32_t r16 = nl - pos;
+    if (((fd + pos) & 15u) == 0u && r16 >= 16u) {
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+    } else {
+      for (uint32_t b = 0; b < 16u && b < r16; ++b) p[b] = (uint8_t)(v[b >> 2] >> (8u * (b & 3u)));
     }
   }
 }
@@ -248,7 +240,8 @@ __global__ __launch_bounds__(kBlock) void mbuf_scatter(ScatterArgs a) {
 
 hipError_t launch_mbuf_scatter(const ScatterArgs &a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(mbuf_scatter, dim3((a.n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(mbuf_scatter, dim3((uint32_t)(((uint64_t)a.n * 16u + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     s, a);
   return hipGetLastError();
 }
 

@@ -334,15 +334,32 @@ impl GpuNat64 {
     /// Rewrite a burst in place in its mbufs (6to4: g::CGPU_NAT64_6TO4,
     /// 4to6: g::CGPU_NAT64_4TO6): the mbufs come back with data_len / pkt_len
     /// adjusted for Act packets and a disposition each, in burst order.
+    /// The burst goes across as (data_address, data_len, tailroom) triples
+    /// read from the headers `rte_eth_rx_burst` has just written
+    /// (cgpu_nat64_frames: the device touches only the frames, in one
+    /// launch sequence and one synchronisation), and the
+    /// lengths are set here as `Mbuf::shrink` / `extend` would leave them
+    /// (mbuf.rs:225-275: data_off unchanged, data_len and pkt_len -20 / +20).
     pub fn nat_burst(&mut self, ctx: &mut GpuContext, direction: u32, mbufs: Vec<Mbuf>)
                      -> (Vec<(Mbuf, GpuDisposition)>, anyhow::Result<()>) {
         let ptrs: Vec<*mut ffi::rte_mbuf> = mbufs.into_iter().map(Mbuf::into_ptr).collect();
         let n = ptrs.len();
+        let mut addrs: Vec<*const u8> = Vec::with_capacity(n);
+        let mut lens: Vec<u16> = Vec::with_capacity(n);
+        let mut tail: Vec<u16> = Vec::with_capacity(n);
+        for &p in &ptrs {
+            // the fields Mbuf::data_address / data_len / tailroom read (mbuf.rs:196-213)
+            let m = unsafe { &*p };
+            addrs.push(unsafe { (m.buf_addr as *const u8).offset(m.data_off as isize) });
+            lens.push(m.data_len);
+            tail.push(m.buf_len - m.data_off - m.data_len);
+        }
+        let mut out_len = vec![0u16; n];
         let mut disp = vec![0u8; n];
         let mut status = vec![0u8; n];
         let rc = check(unsafe {
-            g::cgpu_nat64_mbufs(ctx.0, self.pm, direction, ptrs.as_ptr() as *const *mut c_void,
-                                n as u32, disp.as_mut_ptr(), status.as_mut_ptr())
+            g::cgpu_nat64_frames(ctx.0, self.pm, direction, addrs.as_ptr(), lens.as_ptr(), tail.as_ptr(),
+                                 n as u32, out_len.as_mut_ptr(), disp.as_mut_ptr(), status.as_mut_ptr())
         });
         let out = ptrs
             .into_iter()
@@ -350,7 +367,13 @@ impl GpuNat64 {
             .map(|(i, p)| {
                 let d = match (&rc, disp[i] as u32) {
                     (Err(_), _) => GpuDisposition::Abort(0),
-                    (Ok(()), g::cgpu_disposition::CGPU_ACT) => GpuDisposition::Act,
+                    (Ok(()), g::cgpu_disposition::CGPU_ACT) => {
+                        let m = unsafe { &mut *p };
+                        let grown = out_len[i] as u32 > m.data_len as u32;
+                        m.pkt_len = if grown { m.pkt_len + 20 } else { m.pkt_len - 20 };
+                        m.data_len = out_len[i];
+                        GpuDisposition::Act
+                    }
                     (Ok(()), g::cgpu_disposition::CGPU_DROP) => GpuDisposition::Drop,
                     (Ok(()), _) => GpuDisposition::Abort(status[i] as u32),
                 };
