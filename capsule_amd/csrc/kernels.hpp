@@ -181,7 +181,7 @@ struct ScatterArgs {
   const uint16_t *out_len;
   uint8_t *disposition;   // ACT frames are written; 4to6 without tailroom -> ABORT
   uint8_t *status;
-  const uint64_t *mb_dev;  // nullptr: frame pairs, no mbuf header written
+  const uint64_t *mb_dev;
   const uint64_t *fr_dev;
   const uint32_t *pkt_len;
   const uint32_t *tailroom;
