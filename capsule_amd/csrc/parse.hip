@@ -156,7 +156,7 @@ __device__ __forceinline__ void mask_chunk(u32x4 &v, uint32_t rem) {
 }
 
 // ---- the rows path (L4 checksum configs, waves of long frames) -----------
-// A wave whose frames are 16-B aligned and at least half of them 128 B or
+// A wave whose frames are 16-B aligned and at least 7/8 of them 128 B or
 // longer reads each frame's first 512 B once, in rows: 16 lanes
 // take one 256-B piece of one frame per load instruction (four whole frames
 // per instruction, full lines), sum its u16 words (the frame's last chunk
@@ -280,7 +280,9 @@ __device__ __forceinline__ bool stream_wave(uint32_t off, uint32_t len, bool val
   const uint32_t noff = __shfl_down(off, 1);
   const bool ok = valid && (off & 15u) == 0u && (lane == 63u || (noff > off && noff - off >= len));
   if (__ballot(ok) != ~0ull || !__ballot(len > 96u)) return false;
-  base = __builtin_amdgcn_readfirstlane(off);
+  // the chunk grid starts at the first frame's line: every load instruction
+  // of the stream then covers 8 whole lines, none shared with the next one
+  base = __builtin_amdgcn_readfirstlane(off) & ~127u;
   const uint32_t end = __builtin_amdgcn_readlane(off + len, 63);
   span = end - base;
   return span <= kStreamMax && (uint64_t)end + 16u <= (uint64_t)arena_len;
@@ -293,11 +295,13 @@ struct StreamChunk {
 };
 
 // Chunks at or past `hi` (the end of the half's range) take the owner of
-// chunk hi - 1: a valid frame of the half, whose sum they add 0 to (they are
-// not loaded).  Their own bitmap word may lie past the bitmap.
+// chunk hi - 1, and chunks before `lo` (the line-aligned start of a step
+// grid) the owner of chunk lo: a valid frame of the half, whose sum they add
+// 0 to (they are not loaded).  Their own bitmap word may lie past the bitmap.
 __device__ __forceinline__ StreamChunk stream_chunk(const uint32_t *bm, const uint32_t *pre,
-                                                    const uint32_t *fend, uint32_t c, uint32_t hi) {
-  const uint32_t q = c < hi ? c : hi - 1u, w = q >> 5;
+                                                    const uint32_t *fend, uint32_t c, uint32_t lo,
+                                                    uint32_t hi) {
+  const uint32_t q = c < lo ? lo : (c < hi ? c : hi - 1u), w = q >> 5;
   StreamChunk k;
   k.c = c;
   k.own = pre[w] + (uint32_t)__builtin_popcount(bm[w] & ((2u << (q & 31u)) - 1u)) - 1u;
@@ -327,28 +331,30 @@ __device__ __forceinline__ void stream_prologue(rsrc_t rs, uint32_t base, uint32
   const uint32_t pc = (uint32_t)__builtin_popcount(bm[lane]);
   pre[lane] = wave_scan_incl(pc) - pc;  // frames starting before word `lane`
   const uint32_t nch = (span + 15u) >> 4;
+  const uint32_t first = __builtin_amdgcn_readfirstlane(cs);          // frame 0's first chunk
   const uint32_t mid = __builtin_amdgcn_readlane(cs, (int)kRowHalf);  // half 1's first chunk
 #pragma unroll
   for (uint32_t half = 0; half < 2u; ++half) {
-    const uint32_t lo = half ? mid : 0u, hi = half ? nch : mid;
+    // a half's steps start on the line of its first chunk (base is a line)
+    const uint32_t lo = half ? mid : first, hi = half ? nch : mid;
 #pragma unroll
     for (uint32_t m = 0; m < kRowHalf * kWin / 256u; ++m)
       *reinterpret_cast<u32x4 *>(win + 4u * (64u * m + lane)) = u32x4{0u, 0u, 0u, 0u};
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (uint32_t c0 = lo; c0 < hi; c0 += 64u * kStreamU) {
+    for (uint32_t c0 = lo & ~7u; c0 < hi; c0 += 64u * kStreamU) {
       StreamChunk k[kStreamU];
       u32x4 v[kStreamU];
 #pragma unroll
       for (uint32_t u = 0; u < kStreamU; ++u) {
-        k[u] = stream_chunk(bm, pre, fend, c0 + 64u * u + lane, hi);
+        k[u] = stream_chunk(bm, pre, fend, c0 + 64u * u + lane, lo, hi);
         const uint32_t rel = 16u * k[u].c;
-        const bool in = k[u].c < hi && rel < k[u].fe;
+        const bool in = k[u].c >= lo && k[u].c < hi && rel < k[u].fe;
         v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(in ? base + rel : kNoRead), 0, kNT);
       }
 #pragma unroll
       for (uint32_t u = 0; u < kStreamU; ++u) {
         const uint32_t rel = 16u * k[u].c;
-        const uint32_t rem = k[u].c < hi && rel < k[u].fe ? k[u].fe - rel : 16u;
+        const uint32_t rem = k[u].c >= lo && k[u].c < hi && rel < k[u].fe ? k[u].fe - rel : 16u;
         if (__ballot(rem < 16u)) mask_chunk(v[u], rem);
         // bytes 0..95 of a frame of this half: its window
         const uint32_t pos = rel - fst[k[u].own], fh = k[u].own - kRowHalf * half;
@@ -564,10 +570,11 @@ __device__ __forceinline__ void parse_body(const ParseArgs &a) {
     const bool bad = valid && ((off & 15u) != 0u || (uint64_t)off + len + 16u > (uint64_t)a.arena_len);
     const uint64_t vm = __ballot(valid);
     rows = vm && !__ballot(bad) &&
-           2u * (uint32_t)__popcll(__ballot(valid && len >= 128u)) >= (uint32_t)__popcll(vm);
-    // waves of mostly long frames keep the rows (as fast, fewer VALU per
-    // byte); the stream takes mixed waves (IMIX), whose short frames would
-    // leave 12 of a row's 16 lanes idle
+           8u * (uint32_t)__popcll(__ballot(valid && len >= 128u)) >= 7u * (uint32_t)__popcll(vm);
+    // waves of long frames keep the rows (as fast, fewer VALU per byte); the
+    // stream takes mixed waves (IMIX), whose short frames would leave 12 of a
+    // row's 16 lanes idle, and whose long frames' lines past byte 512 the
+    // rows' tail pass would fetch a second time
     stream = !rows && stream_wave(off, len, valid, threadIdx.x & 63u, a.arena_len, st_base, st_span);
   }
   const bool slow = (off & 3u) != 0u || (uint64_t)off + 96u > (uint64_t)a.arena_len;

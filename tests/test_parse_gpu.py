@@ -483,3 +483,29 @@ def test_stream_path_64b_slots(ctx, seed):
         ln = np.array([len(f) for f in fr], np.uint16)
         om = assert_parity(ctx, arena, np.array(off, np.uint32), ln, ALL)
         assert (om & N.META_L4_CSUM_OK).all()
+
+
+@pytest.mark.parametrize("k", [32, 48, 55, 56, 64])
+def test_stream_rows_threshold(ctx, k):
+    """Waves of k 500-B frames (512-B slots) among 64 - k 64-B ones, the long
+    frames 64 B into a 128-B line so that spans start mid-line: k < 56 take
+    the stream path (its chunk grid starts at the first frame's line), k >= 56
+    (7/8 of the wave) the rows path; each wave's frames shuffled: bit-exact."""
+    rng = np.random.default_rng(100 + k)
+    fr, off, o = [], [], 64
+    for w in range(32):
+        longs = set(rng.choice(64, k, replace=False).tolist())
+        for j in range(64):
+            L = 500 if j in longs else 64
+            kind = ((synth.V6_TCP, synth.V4_UDP, synth.V4_TCP, synth.V6_UDP)[(w + j) % 4] if L == 500
+                    else (synth.V4_UDP, synth.V4_TCP)[(w + j) % 2])
+            fr.append(bytes(synth.build_frames(rng, 1, kind, L, 0)[0]))
+            off.append(o)
+            o += 512 if L == 500 else 64
+    arena = np.full(o + 16, 0x5a, np.uint8)
+    for a0, f in zip(off, fr):
+        arena[a0:a0 + len(f)] = np.frombuffer(f, np.uint8)
+    ln = np.array([len(f) for f in fr], np.uint16)
+    assert 128 <= len(arena) // len(fr) <= 2200  # the variant with both paths
+    om = assert_parity(ctx, arena, np.array(off, np.uint32), ln, ALL)
+    assert (om & N.META_L4_CSUM_OK).all()
