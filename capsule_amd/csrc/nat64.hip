@@ -331,11 +331,13 @@ __device__ __forceinline__ uint32_t probe_port_at(const Nat64Args &a, uint32_t i
       }
     } else if (stag == tag) {
       // joined on the tag alone: the key goes to the stash; the key's first
-      // packet index (w[7] only decreases, so a value loaded with the slot
-      // that is already below i makes the atomic moot)
+      // packet index.  w[7] only decreases and never exceeds the claimer's
+      // index (ref - 1), so a packet after the claimer, or after a w[7]
+      // loaded with the slot, needs no atomic: with the packets probing in
+      // about their own order, most joiners of a key skip it
       a.stash_key[i] = u32x4{key[0], key[1], key[2], key[3]};
       a.stash_port[i] = (uint16_t)key[4];
-      if (s1[3] > i) atomicMin(&w[7], i);
+      if (s1[3] > i && i + 1u < ref) atomicMin(&w[7], i);
       return h | kLocalBit;
     }
     h = (h + 1u) & a.pm.cap_mask;
@@ -1218,6 +1220,11 @@ __device__ __forceinline__ bool stash_matches(const Nat64Args &a, uint32_t i, co
 __device__ __forceinline__ uint32_t pkt_slot_of(const Nat64Args &a, uint32_t i) {
   return a.wave_flag[i / kRowFrames] ? a.pkt_slot[i] : kNoSlot;
 }
+// The same inside the repair, which rewrites entries (thread 0) that the
+// workgroup's other threads then read: at the coherence point.
+__device__ __forceinline__ uint32_t pkt_slot_sc1(const Nat64Args &a, uint32_t i) {
+  return a.wave_flag[i / kRowFrames] ? ld_sc1(&a.pkt_slot[i]) : kNoSlot;
+}
 
 // One chunk's first packets (all kBlock threads): the mask words and the
 // count, sc1.  Tag-joined packets whose key is not their slot's (collisions)
@@ -1228,13 +1235,14 @@ __device__ __forceinline__ void chunk_firsts(const Nat64Args &a, uint32_t c, boo
                                              const TailCtl &ctl) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t i = c * kBlock + threadIdx.x;
-  const uint32_t ps = i < a.n ? pkt_slot_of(a, i) : kNoSlot;
+  const uint32_t ps = i < a.n ? pkt_slot_sc1(a, i) : kNoSlot;
   const bool loc = ps != kNoSlot && (ps & kLocalBit);
   bool bad = false, f = false;
   if (loc) {
     const uint32_t *w = a.pm.slots[ps & kSlotMask].w;
     if (verify && !(ps & kClaimBit)) bad = !stash_matches(a, i, w);
-    f = !bad && w[7] == i;
+    // w[7] as the repair left it, at the coherence point (its atomics)
+    f = !bad && ld_sc1(&w[7]) == i;
   }
   const uint64_t m = __ballot(f);
   if (lane == 0) {
@@ -1403,17 +1411,34 @@ __device__ void tail_repair(const Nat64Args &a, uint32_t nb, uint32_t nmism, con
   }
   __syncthreads();
   // 2. the first packet of each slot a collision had joined: the minimum
-  // over the packets that belong to it now
+  // over the packets that belong to it now.  More such slots than the set
+  // holds (s_all): the first packet of every slot of the batch is computed
+  // again, from all packets (a slot outside the set would otherwise keep a
+  // first packet that has moved to another slot, and its key no port).
   const uint32_t ns = s_ns;
-  for (uint32_t i = threadIdx.x; i < a.n; i += kBlock) {
-    const uint32_t ps = pkt_slot_of(a, i);
-    if (ps == kNoSlot || !(ps & kLocalBit)) continue;
-    const uint32_t sl = ps & kSlotMask;
-    for (uint32_t k = 0; k < ns; ++k)
-      if (s_slot[k] == sl) atomicMin(&s_min[k], i);
+  if (s_all) {
+    for (uint32_t i = threadIdx.x; i < a.n; i += kBlock) {
+      const uint32_t ps = pkt_slot_sc1(a, i);
+      if (ps != kNoSlot && (ps & kLocalBit)) st_sc1(&a.pm.slots[ps & kSlotMask].w[7], 0xffffffffu);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < a.n; i += kBlock) {
+      const uint32_t ps = pkt_slot_sc1(a, i);
+      if (ps != kNoSlot && (ps & kLocalBit)) atomicMin(&a.pm.slots[ps & kSlotMask].w[7], i);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+  } else {
+    for (uint32_t i = threadIdx.x; i < a.n; i += kBlock) {
+      const uint32_t ps = pkt_slot_of(a, i);
+      if (ps == kNoSlot || !(ps & kLocalBit)) continue;
+      const uint32_t sl = ps & kSlotMask;
+      for (uint32_t k = 0; k < ns; ++k)
+        if (s_slot[k] == sl) atomicMin(&s_min[k], i);
+    }
   }
   __syncthreads();
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0 && !s_all)
     for (uint32_t k = 0; k < ns; ++k) {
       a.pm.slots[s_slot[k]].w[7] = s_min[k];
       const uint32_t ch = s_min[k] / kBlock;

@@ -554,3 +554,30 @@ def test_cold_batch_past_the_tails_single_round(ctx):
         _nat_both(ctx, gw, pm, "6to4", a, o, l, o, len(a) + 64)
         assert gw.size() == pm.size() and gw.next_port() == pm.next_port()
     gw.close()
+
+
+@pytest.mark.parametrize("n", [60_000, 70_000])
+def test_repair_set_overflow(tctx, monkeypatch, n):
+    """More colliding slots than the tail's repair set holds (kRepairSet):
+    with one claim-tag bit kept (test build) about half of 3,300 keys meet a
+    batch-local slot of another key with their tag.  The repair then computes
+    the first packet of every slot of the batch again from all packets (a
+    slot outside the set kept a first packet that had moved elsewhere, and
+    its key got no port: round 6).  Drops and truncated frames, a map at load
+    0.4; every byte, length, disposition, status and the map state equal the
+    oracle's on the first call, again after a reset, and on a steady call."""
+    from capsule_amd import packets
+
+    monkeypatch.setenv("CGPU_TEST_NAT64_TAG_MASK", "0x1")
+    gw = packets.Nat64Gateway(tctx, capacity_log2=13)  # 8192 slots
+    monkeypatch.delenv("CGPU_TEST_NAT64_TAG_MASK")
+    a, o, l = synth.nat64_stream(70_000, n_keys=3300, seed=95, drop_frac=0.05)
+    a, o, l = a[:int(o[n - 1]) + 256], o[:n], l[:n]
+    pm = oracle_lib.PortMap()
+    for reset in (False, True, False):
+        if reset:
+            gw.reset()
+            pm = oracle_lib.PortMap()
+        _nat_both(tctx, gw, pm, "6to4", a, o, l, o, len(a) + 64)
+        assert gw.size() == pm.size() and gw.next_port() == pm.next_port()
+    gw.close()
