@@ -190,7 +190,7 @@ unsigned long long sched_key(void *stream) {
 }
 
 // Gives a call of a.n frames on `stream` its wave schedule when the launch
-// is more than one round of waves: the last min(groups - resident,
+// is more than one round of waves: the last min(groups - resident / 2,
 // kSchedMax) groups of 64 frames, rounded down to whole lists of 256, are
 // ordered longest span first (parse.hip).  The kernel ignores it unless it
 // runs the rows variant.  The schedule is an optimisation, never needed for
@@ -203,8 +203,12 @@ void set_schedule(cgpu_ctx *c, cgpu::ParseArgs &a, void *stream) {
   a.sched_spins = c->sched_spins;
   const uint32_t groups = (a.n + 63u) / 64u;
   if (c->resident_waves == 0 || groups <= c->resident_waves) return;
-  // whole lists of 256 groups (one ordering workgroup each)
-  const uint32_t over = groups - c->resident_waves;
+  // Every group after the first half round is ordered (whole lists of 256
+  // groups, one ordering workgroup each): the second half of the first
+  // round's waves then take the longest groups too (IMIX with checksums
+  // 77.6-78.1 -> 75.8-76.2 us against ordering from the second round on,
+  // DESIGN.md section 3.1).
+  const uint32_t over = groups - c->resident_waves / 2u;
   const uint32_t n_sched = (over < cgpu::kSchedMax ? over : cgpu::kSchedMax) / 256u * 256u;
   if (n_sched == 0) return;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;

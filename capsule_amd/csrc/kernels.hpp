@@ -49,7 +49,7 @@ struct ParseArgs {
 // Waves the rows kernels keep resident per CU (8 waves per SIMD), and the
 // most waves one launch orders (the granules of one schedule buffer).
 constexpr uint32_t kResidentWavesPerCU = 32;
-constexpr uint32_t kSchedMax = 8192;
+constexpr uint32_t kSchedMax = 16384;
 // Granule polls before a wave gives up (each poll sleeps ~0.5 us: seconds,
 // against the microseconds the ordering workgroups take; DESIGN.md §3.1
 // "Forward progress").

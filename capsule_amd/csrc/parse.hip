@@ -385,14 +385,15 @@ __device__ __forceinline__ void stream_prologue(rsrc_t rs, uint32_t base, uint32
   s_all = acc[lane];
 }
 
-// ---- Longest span first: the order of the last round of waves ------------
+// ---- Longest span first: the order of the later waves ---------------------
 // A wave takes 64 consecutive frames, and on the stream / rows paths its time
 // follows its span (the bytes from its first frame's start to its last
 // frame's end): for shuffled IMIX 11 to 37 KB.  A 1 Mi-packet launch is
 // 16,384 waves, two per wave slot of the chip, and the waves dispatched last
 // decide when it ends: with the groups taken in their own order the launch
-// took 86.7 us, with the last half of them taken longest span first 77.3 us
-// (tools/imix_order_probe.py).  So the launch's first
+// took 86.7 us, with the last half of them taken longest span first 77.3 us,
+// with all after the first quarter 76.5 us (tools/imix_order_probe.py,
+// DESIGN.md section 3.1; the host orders from half a round on).  So the launch's first
 // sched_n / 256 workgroups each order 256 of the last sched_n groups by span,
 // longest first (64 classes a quarter octave wide; a counting sort in LDS,
 // one atomic per class present in a wave, never one per lane), and the k-th

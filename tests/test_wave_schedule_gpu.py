@@ -7,8 +7,9 @@ The bench-size batches (1 Mi frames, 16,384 groups against 8,192 resident
 waves) take the schedule in tests/test_bench_parity_gpu.py and
 tests/test_reconcile_gpu.py.  Here the test build's hook CGPU_TEST_SCHED_WAVES
 (read when a context is created) makes small batches take it: with 256
-resident waves, a batch of 600 groups has its last 256 ordered (whole
-lists of 256 groups, one ordering workgroup each).  Covered:
+resident waves, the groups after the first 128 (half a round) are ordered,
+in whole lists of 256 groups (one ordering workgroup each): a batch of 600
+groups has its last 256 ordered.  Covered:
 IMIX (stream path), 256-B and 1500-B frames (rows path), out-of-order
 descriptors (window path; the scheduler's lightest class), a partial last
 group, reconcile on stale IMIX, more groups than one schedule holds, two
@@ -100,9 +101,10 @@ def test_groups_out_of_order(sctx):
 
 
 def test_more_groups_than_one_schedule(sctx):
-    """256 resident waves, 8,192 ordered at most: a batch of 9,000 groups
-    runs groups 256 .. 807 in their own order and orders the last 8,192."""
-    arena, off, ln = synth.imix(64 * 9000, seed=5)
+    """256 resident waves, 16,384 ordered at most (from half a round on): a
+    batch of 17,000 groups runs groups 0 .. 615 in their own order and
+    orders the last 16,384."""
+    arena, off, ln = synth.imix(64 * 17000, seed=5)
     _check_parse(sctx, arena, off, ln)
 
 
