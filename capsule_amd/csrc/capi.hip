@@ -132,6 +132,10 @@ struct cgpu_ctx {
     unsigned long long key;
     unsigned long long *buf;
     uint32_t tag;
+    // whether the stream's latest ordered batch had spans of more than one
+    // class (written by its first ordering workgroup; 1 until then)
+    volatile uint32_t *spread_h;
+    uint32_t *spread_d;
   };
   std::vector<Sched> sched;
 };
@@ -180,7 +184,23 @@ cgpu_ctx::Sched *sched_buffer(cgpu_ctx *c, unsigned long long key, hipStream_t s
     (void)hipFree(buf);
     return nullptr;
   }
-  c->sched.push_back(cgpu_ctx::Sched{key, buf, 0u});
+  // the spread word: page-locked and mapped (nullptr if it cannot be had:
+  // every batch is then taken to vary)
+  void *h = nullptr;
+  uint32_t *d = nullptr;
+  if (hipHostMalloc(&h, 4, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+    *(volatile uint32_t *)h = 1u;
+    if (hipHostGetDevicePointer((void **)&d, h, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipHostFree(h);
+      h = nullptr;
+      d = nullptr;
+    }
+  } else {
+    (void)hipGetLastError();
+    h = nullptr;
+  }
+  c->sched.push_back(cgpu_ctx::Sched{key, buf, 0u, (volatile uint32_t *)h, d});
   return &c->sched.back();
 }
 
@@ -199,18 +219,11 @@ unsigned long long sched_key(void *stream) {
 // allocated leaves the call unordered.
 void set_schedule(cgpu_ctx *c, cgpu::ParseArgs &a, void *stream) {
   a.sched = nullptr;
+  a.sched_spread = nullptr;
   a.dev_err = c->dev_err;
   a.sched_spins = c->sched_spins;
   const uint32_t groups = (a.n + 63u) / 64u;
   if (c->resident_waves == 0 || groups <= c->resident_waves) return;
-  // Every group after the first half round is ordered (whole lists of 256
-  // groups, one ordering workgroup each): the second half of the first
-  // round's waves then take the longest groups too (IMIX with checksums
-  // 77.6-78.1 -> 75.8-76.2 us against ordering from the second round on,
-  // DESIGN.md section 3.1).
-  const uint32_t over = groups - c->resident_waves / 2u;
-  const uint32_t n_sched = (over < cgpu::kSchedMax ? over : cgpu::kSchedMax) / 256u * 256u;
-  if (n_sched == 0) return;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) {
     (void)hipGetLastError();
@@ -219,7 +232,21 @@ void set_schedule(cgpu_ctx *c, cgpu::ParseArgs &a, void *stream) {
   if (cs != hipStreamCaptureStatusNone) return;
   cgpu_ctx::Sched *b = sched_buffer(c, sched_key(stream), (hipStream_t)stream);
   if (!b) return;
+  // Every group after the first half round is ordered (whole lists of 256
+  // groups, one ordering workgroup each): the second half of the first
+  // round's waves then take the longest groups too (IMIX with checksums
+  // 77.6-78.1 -> 75.8-76.2 us against ordering from the second round on,
+  // DESIGN.md section 3.1).  Those waves wait for the order, which buys
+  // nothing when every group has one span (256-B frames: +1-2 us): when the
+  // stream's latest ordered batch was such, only the groups after the first
+  // round are ordered.  (A guess from the previous batch, read without a
+  // synchronisation; results never depend on it.)
+  const bool spread = b->spread_h == nullptr || *b->spread_h != 0u;
+  const uint32_t over = groups - (spread ? c->resident_waves / 2u : c->resident_waves);
+  const uint32_t n_sched = (over < cgpu::kSchedMax ? over : cgpu::kSchedMax) / 256u * 256u;
+  if (n_sched == 0) return;
   if (++b->tag == 0u) b->tag = 1u;  // tags are never 0: a zeroed granule matches no call
+  a.sched_spread = b->spread_d;
   a.sched = b->buf;
   a.sched_n = n_sched;
   a.sched_from = groups - n_sched;
@@ -382,7 +409,10 @@ void cgpu_ctx_destroy(cgpu_ctx *c) {
   if (c->h_desc) (void)hipHostFree(c->h_desc);
   if (c->d_desc) (void)hipFree(c->d_desc);
   if (c->gb_counts) (void)hipFree(c->gb_counts);
-  for (auto &x : c->sched) (void)hipFree(x.buf);
+  for (auto &x : c->sched) {
+    (void)hipFree(x.buf);
+    if (x.spread_h) (void)hipHostFree((void *)x.spread_h);
+  }
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_zc) (void)hipFree(c->d_zc);
   for (uint32_t r = 0; r < c->nreg; ++r)

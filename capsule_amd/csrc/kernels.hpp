@@ -44,6 +44,10 @@ struct ParseArgs {
   // entry points report as CGPU_EIO).
   uint32_t sched_spins = 0;
   uint32_t *dev_err = nullptr;
+  // Optional (page-locked host word, device mapping): the first ordering
+  // workgroup writes whether its groups' spans fall in more than one class,
+  // which the host reads when it sizes the stream's next schedule.
+  uint32_t *sched_spread = nullptr;
 };
 
 // Waves the rows kernels keep resident per CU (8 waves per SIMD), and the

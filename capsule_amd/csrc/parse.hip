@@ -461,6 +461,13 @@ __device__ void schedule_waves(const ParseArgs &a, uint32_t *L) {
   __syncthreads();
   if (t < 64u) {  // exclusive prefix over the classes (one wave, 64 classes)
     const uint32_t x = cnt[t];
+    // the first list tells the host whether this batch's spans vary (one
+    // class: the order buys nothing, and the host orders the stream's next
+    // batch from the second round on only, so that no first-round wave waits)
+    const uint64_t present = __ballot(x != 0u);
+    if (blockIdx.x == 0 && t == 0 && a.sched_spread != nullptr)
+      __hip_atomic_store(a.sched_spread, __popcll(present) > 1 ? 1u : 0u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t y = x;
 #pragma unroll
     for (uint32_t d = 1; d < 64u; d <<= 1) {

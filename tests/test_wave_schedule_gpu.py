@@ -230,3 +230,15 @@ def test_give_up_is_reported():
         c.check()
     finally:
         c.close()
+
+
+def test_order_range_follows_the_previous_batch(sctx):
+    """The host orders from half a round on after a batch whose spans vary,
+    from the second round on after one whose groups all have one span (the
+    first ordering workgroup's report, capi.hip set_schedule).  Uniform and
+    IMIX batches alternating on one stream: every result exact, whichever
+    range each call gets."""
+    imix = synth.imix(64 * 700, seed=21)
+    uni = synth.uniform(64 * 700, frame_len=256, slot=256, seed=22)
+    for arena, off, ln in (uni, imix, uni, uni, imix, imix, uni):
+        _check_parse(sctx, arena, off, ln)
