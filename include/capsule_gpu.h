@@ -257,8 +257,9 @@ int cgpu_ctx_check(cgpu_ctx *ctx, void *stream);
  * as they are, and the hash of Udp/Tcp::flow() (udp.rs:151, tcp.rs:409).
  * Asynchronous on `stream`.  A batch of more than one round of waves (64
  * frames a wave, 32 waves resident per CU) with checksums over long frames
- * orders its waves after the first half round longest span first through a
- * 128 KB buffer the
+ * orders its later waves longest span first (from half a round on when the
+ * stream's previous ordered batch had spans that vary, else from the second
+ * round on) through a 128 KB buffer the
  * context keeps per stream (allocated by the first such call on a stream
  * and zeroed on that stream; no device-wide synchronisation).  A call made
  * while its stream is being captured into a graph runs without the order
